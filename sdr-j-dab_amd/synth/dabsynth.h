@@ -1,0 +1,71 @@
+/*
+ * dabsynth.h -- synthetic DAB Mode-I transmitter (input generator for the
+ * tests and bench; not part of the decode path).
+ *
+ * sdr-j-dab has no signal generator (its GENERATOR device id is declared
+ * but unimplemented, virtual-input.h:41), so this is the build's own
+ * ETSI EN 300 401 Mode-I modulator: FIBs with CRC, energy dispersal,
+ * k=7 R=1/4 convolutional code, FIC/MSC puncturing (UEP and EEP), time
+ * interleaving, CIF assembly, frequency interleaving, DQPSK against the
+ * phase reference symbol, IFFT, cyclic prefix, null symbol, AWGN and CFO.
+ * Its conventions are the inverse of the reference receiver's:
+ *   soft bit i of a symbol  -> carrier i real part, bit 1536+i -> imag part
+ *   QPSK  (1-2b_re) + j(1-2b_im), DQPSK z_l[k] = z_{l-1}[k] * q
+ *   time interleaving delay 15 - d(i) so the receiver's d(i) makes 15
+ *   (receiver CIF n decodes encoder CIF n-15).
+ */
+#ifndef DABSYNTH_H
+#define DABSYNTH_H
+#include <stdint.h>
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct {
+    int16_t startAddr;   /* CU address 0..863 */
+    int16_t length;      /* subchannel size in CUs */
+    int16_t bitRate;     /* kbit/s */
+    int16_t protLevel;   /* UEP level 1..5, or EEP 0100|lvl (A) / 0200|lvl (B) */
+    int16_t uep;         /* 1 = UEP (uepFlag 0 in the reference), 0 = EEP */
+    int16_t dabplus;     /* 1: payload is a DAB+ superframe stream with valid RS/fire code */
+} dabsynth_subch;
+
+typedef struct {
+    int32_t n_frames;    /* frames after the pre-roll */
+    int32_t pre_offset;  /* stream starts this many samples into a pre-roll frame */
+    float   snr_db;      /* >= 200: noiseless */
+    float   cfo_hz;      /* carrier frequency offset */
+    float   amplitude;   /* RMS of the OFDM signal */
+    int32_t n_subch;
+    const dabsynth_subch *subch;
+} dabsynth_cfg;
+
+/* total stream length in samples */
+int64_t dabsynth_stream_len(const dabsynth_cfg *cfg);
+/* Generate one ensemble.  iq: cf32[stream_len].  Optional truth outputs:
+ *   fic_bits   [n_frames][4][768]     FIB bits (CRC field as transmitted)
+ *   msc_bits   [4*n_frames][n_subch][24*max_bitRate]  info bits the receiver
+ *              must output at CIF n (valid for n >= 16)
+ *   coded_bits [n_frames][75][3072]  hard bits carried by each data symbol
+ *   frame0_start  stream index of frame 0's null symbol start
+ * returns 0 on success. */
+int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
+                      uint8_t *fic_bits, uint8_t *msc_bits, uint8_t *coded_bits,
+                      int64_t *frame0_start);
+
+/* Many ensembles in parallel (host threads).  iq: [n_ens][stream_len]; the
+ * truth pointers may be NULL; seeds are seed0 + ensemble index. */
+int dabsynth_generate_many(const dabsynth_cfg *cfg, uint64_t seed0, int n_ens, int n_threads,
+                           float *iq, uint8_t *fic_bits, uint8_t *msc_bits);
+
+/* building blocks exposed for tests */
+void dabsynth_conv_encode(const uint8_t *bits, int nbits, uint8_t *coded /*[4*(nbits+6)]*/);
+int  dabsynth_puncture_msc(int uep, int bitRate, int protLevel, const uint8_t *mother, uint8_t *out);
+void dabsynth_puncture_fic(const uint8_t *mother /*[3096]*/, uint8_t *out /*[2304]*/);
+void dabsynth_make_fib(uint64_t *rng_state, uint8_t *fib /*[256]*/);
+void dabsynth_rs_encode(const uint8_t *data /*[110]*/, uint8_t *cw /*[120]*/);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
