@@ -1,0 +1,207 @@
+/*
+ * dabgpu.h -- C ABI of the MI355X-native DAB Mode-I demod/decode path.
+ *
+ * Plain C: pointers, sizes and PODs only (no HIP or torch types), so a C++
+ * drop-in for sdr-j-dab's ofdmProcessor / ficHandler / mscHandler, a ctypes
+ * or a cgo binding can all call it.  Every entry point names the reference
+ * interface it replaces (paths relative to the sdr-j-dab v0.997 tree).
+ *
+ * Conventions
+ *  - return value: 0 on success, a negative DABGPU_E* code on failure; the
+ *    message of the last failure on this thread is dabgpu_last_error().
+ *    No C++ exception crosses this boundary.
+ *  - "_d" pointers are device (HBM) pointers obtained from dabgpu_alloc or
+ *    any HIP allocation on the context's device; "_h" pointers are host.
+ *  - every device-side call is asynchronous on the context's stream;
+ *    dabgpu_sync() waits.  Calls that return host data synchronise.
+ *  - one context per calling thread (contexts are independent streams).
+ *  - data formats follow the reference: IQ is interleaved cf32 (re, im)
+ *    scaled to about +-1 (virtual-input.h:51-70); soft bits are int16 in
+ *    [-127, 127] (ofdm-decoder.cpp:186-189); decoded bits are one bit per
+ *    uint8 (viterbi.cpp:240-241).
+ */
+#ifndef DABGPU_H
+#define DABGPU_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DABGPU_ABI_VERSION 1
+
+/* error codes */
+#define DABGPU_OK          0
+#define DABGPU_E_ARG      -1   /* invalid argument / shape */
+#define DABGPU_E_HIP      -2   /* HIP runtime error */
+#define DABGPU_E_NODEV    -3   /* no usable gfx950 device */
+#define DABGPU_E_NOMEM    -4
+#define DABGPU_E_UNSUP    -5   /* configuration the reference does not define */
+#define DABGPU_E_STATE    -6   /* call out of sequence */
+
+/* Mode-I geometry (gui.cpp:1361-1371) */
+#define DABGPU_TU     2048
+#define DABGPU_TS     2552
+#define DABGPU_TG     504
+#define DABGPU_TNULL  2656
+#define DABGPU_TF     196608
+#define DABGPU_K      1536
+#define DABGPU_L      76
+#define DABGPU_CIF_BITS 55296
+
+typedef struct dabgpu_ctx dabgpu_ctx;
+
+/* Subchannel of the MSC, as produced by the FIB parser (dab-constants.h:151-176,
+ * audiodata/packetdata: startAddr, length in CUs, uepFlag, protLevel, bitRate).
+ * uepFlag == 0 selects UEP (deconvolve.cpp:130); otherwise protLevel carries
+ * 0100|level (EEP-A) or 0200|level (EEP-B). */
+typedef struct {
+    int16_t startAddr;
+    int16_t length;
+    int16_t bitRate;
+    int16_t protLevel;
+    int16_t uepFlag;
+    int16_t reserved;
+} dabgpu_subch;
+
+/* Per-frame front-end parameters (ofdm-processor.cpp:344-446), one per
+ * (stream, frame).  Sample indices are relative to the stream's base.
+ * The NCO follows getSamples: for the k-th sample read in a segment
+ * (k = 1, 2, ...), localPhase = (lp - k*phase) mod 2048000 and the
+ * sample is multiplied by oscillatorTable[localPhase]. */
+typedef struct {
+    int64_t iq_base;    /* element offset (cf32 units) of the stream in the IQ buffer */
+    int64_t window;     /* first sample of the T_u sync window (SyncOnPhase) */
+    int64_t block0;     /* first sample of block 0 = window + startIndex */
+    int32_t lp_window;  /* localPhase before the window's first sample */
+    int32_t phase_a;    /* coarse+fine while reading window and PRS (segment A) */
+    int32_t lp_data;    /* localPhase before the first data-symbol sample */
+    int32_t phase_b;    /* coarse+fine while reading symbols 1..75 (segment B) */
+    int32_t out_slot;   /* output frame slot in the soft-bit buffer */
+    int32_t flags;      /* bit0: run coarse AFC (f2Correction) in block0 */
+} dabgpu_frame;
+
+/* ---- context ---------------------------------------------------------- */
+int         dabgpu_abi_version(void);
+const char *dabgpu_last_error(void);
+int         dabgpu_device_count(void);
+int         dabgpu_ctx_create(int device, dabgpu_ctx **out);
+int         dabgpu_ctx_destroy(dabgpu_ctx *ctx);
+int         dabgpu_sync(dabgpu_ctx *ctx);
+int         dabgpu_alloc(dabgpu_ctx *ctx, size_t bytes, void **dptr);
+int         dabgpu_free(dabgpu_ctx *ctx, void *dptr);
+int         dabgpu_memcpy_h2d(dabgpu_ctx *ctx, void *dst_d, const void *src_h, size_t bytes);
+int         dabgpu_memcpy_d2h(dabgpu_ctx *ctx, void *dst_h, const void *src_d, size_t bytes);
+int         dabgpu_memset_d(dabgpu_ctx *ctx, void *dst_d, int value, size_t bytes);
+/* HIP events on the context stream, for timing (ms between two marks) */
+int         dabgpu_event_record(dabgpu_ctx *ctx, int slot);
+int         dabgpu_event_elapsed(dabgpu_ctx *ctx, int slot_a, int slot_b, float *ms);
+
+/* ---- OFDM front end (L3) ---------------------------------------------- */
+
+/* phaseReference::findIndex batched (phasereference.cpp:60-88): for each of n
+ * frames, FFT of the NCO-mixed T_u window, x conj(PRS), IFFT, argmax |.|.
+ * start_index[i] follows the reference: argmax, or -|Max/mean|-1 (truncated)
+ * when Max < level*mean.  maxv/sumv (optional) receive Max and sum |.|. */
+int dabgpu_prs_sync(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n,
+                    int16_t level, int32_t *start_index_d, float *maxv_d, float *sumv_d);
+
+/* ofdmDecoder::processBlock_0 batched (ofdm-decoder.cpp:85-127, freqSyncMethod 1):
+ * FFT of block 0; when frames[i].flags&1 the coarse offset estimate, else 0. */
+int dabgpu_block0(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n,
+                  int16_t *correction_d);
+
+/* ofdmDecoder::processToken for symbols 1..75 of n frames (ofdm-decoder.cpp:167-190):
+ * FFT, x conj(previous symbol), frequency de-interleave (mapper.cpp:115),
+ * ibits = (int16)(-re/(|re|+|im|)*127).  Output layout
+ *   softbits_d[out_slot][75][3072]  (FIC = symbols 1..3, CIF c = symbols 4+18c..21+18c)
+ * softf_d (optional, same layout, float -re/|.|, -im/|.|) for parity tests.
+ * freqcorr_d (optional) float2[n]: sum over the frame of x[i]*conj(x[i-T_u]),
+ * i in [T_u, T_s) (ofdm-processor.cpp:424-438), in unspecified float order. */
+int dabgpu_ofdm_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n,
+                      int16_t *softbits_d, float *softf_d, float *freqcorr_d);
+
+/* ---- channel decoding (L4) -------------------------------------------- */
+
+/* viterbi::deconvolve batched (viterbi.cpp:225-242): n_cw codewords of
+ * 4*(nbits+6) depunctured soft bits -> nbits decoded bits each. */
+int dabgpu_viterbi(dabgpu_ctx *ctx, const int16_t *in_d, int n_cw, int nbits, uint8_t *out_d);
+
+/* ficHandler::process_ficInput batched (fic-handler.cpp:241-321): n blocks of
+ * 2304 soft bits (contiguous, block stride 2304) -> 768 bits after energy
+ * dispersal, with each FIB's CRC field inverted by the check exactly as
+ * check_CRC_bits leaves it (dab-constants.h:316-317); crc_ok_d[3*n]. */
+int dabgpu_fic_decode(dabgpu_ctx *ctx, const int16_t *fic_soft_d, int n, uint8_t *bits_d,
+                      uint8_t *crc_ok_d);
+
+/* FIC blocks straight from a demod soft-bit buffer: frames slots[0..n_frames)
+ * each give 4 blocks (symbols 1..3 of the slot). Output [n_frames][4][768]. */
+int dabgpu_fic_decode_frames(dabgpu_ctx *ctx, const int16_t *softbits_d, const int32_t *slots_h,
+                             int n_frames, uint8_t *bits_d, uint8_t *crc_ok_d);
+
+/* uep_/eep_deconvolve::deconvolve + energy dispersal (deconvolve.cpp:172-237,
+ * 325-366; dab-concurrent.cpp:183-190) for n_cw codewords whose
+ * fragmentSize = length*64 soft bits are given contiguous (already
+ * time-de-interleaved), one subchannel description per codeword.
+ * Output bits_d[n_cw][24*max_bitRate] (row stride out_stride bytes). */
+int dabgpu_msc_deconvolve(dabgpu_ctx *ctx, const int16_t *frag_d, int64_t frag_stride,
+                          const dabgpu_subch *subch_h, int n_cw, uint8_t *bits_d, int64_t out_stride);
+
+/* ---- streaming pipeline (ofdmProcessor::run + ficHandler + mscHandler) ---
+ * n_streams independent ensembles; each call decodes n_frames frames per
+ * stream.  Sync, AFC, DQPSK references and the 16-CIF time de-interleaver
+ * state (dab-concurrent.cpp:162-175: the first 16 CIFs are warm-up) are
+ * carried across calls.  subch lists the subchannels decoded for every
+ * stream (the reference decodes one selected subchannel; this decodes all). */
+typedef struct dabgpu_pipe dabgpu_pipe;
+typedef struct {
+    int32_t n_streams;
+    int32_t n_frames;          /* frames per dabgpu_pipe_run call */
+    int32_t n_subch;
+    int16_t threshold;         /* findIndex level (gui.cpp:98-99, default 3) */
+    int16_t freq_sync_method;  /* only 1 (main.cpp:91 default) is implemented */
+    const dabgpu_subch *subch;
+} dabgpu_pipe_cfg;
+
+typedef struct {
+    int64_t next_pos;          /* stream index of the next window (SyncOnPhase) */
+    int32_t local_phase;
+    int32_t coarse;            /* coarseCorrector */
+    int16_t fine;              /* fineCorrector */
+    int16_t f2correction;
+    int16_t prev1, prev2;
+    int32_t synced;
+    int64_t cif_count;         /* CIFs delivered to the MSC so far */
+    int32_t last_start_index;
+    int32_t resyncs;
+} dabgpu_stream_state;
+
+int dabgpu_pipe_create(dabgpu_ctx *ctx, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **out);
+int dabgpu_pipe_destroy(dabgpu_pipe *p);
+/* Acquire (notSynced/SyncOnNull/SyncOnEndNull, ofdm-processor.cpp:274-338)
+ * every stream from sample start_h[s] of its IQ (device, stream s at iq_d +
+ * 2*stream_stride*s, n_avail_h[s] samples). */
+int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride,
+                        const int64_t *start_h, const int64_t *n_avail_h);
+/* Decode the next n_frames frames of every stream.  Outputs (device):
+ *   fic_bits_d  [n_streams][n_frames][4][768], fic_crc_d [n_streams][n_frames][12]
+ *   msc_bits_d  [n_streams][4*n_frames][n_subch][msc_stride] (24*bitRate used)
+ *   msc_valid_h [n_streams][4*n_frames] (host, optional): 1 where the CIF is
+ *               past the 16-CIF warm-up.
+ * Returns 0, or DABGPU_E_STATE if a stream lost sync (see dabgpu_pipe_state). */
+int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, const int64_t *n_avail_h,
+                    uint8_t *fic_bits_d, uint8_t *fic_crc_d, uint8_t *msc_bits_d, int32_t msc_stride,
+                    uint8_t *msc_valid_h);
+int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
+/* device soft-bit ring of the last run ([n_streams][ring][75][3072]) and the slot of
+ * (stream, frame) in it, for tests */
+int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft_d, int32_t *ring_frames);
+int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot);
+/* per-frame front-end record of the last run: [n_streams][n_frames] */
+int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *frames_h, int32_t *start_index_h);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,99 @@
+// dab_kernels.h -- host/device shared structs and kernel launchers.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "../../include/dabgpu.h"
+
+namespace dab {
+
+constexpr int TU = 2048, TS = 2552, TG = 504, TNULL = 2656, TF = 196608, K = 1536, L = 76;
+constexpr int NSYM = 75;                 // data symbols per frame
+constexpr int SYMBITS = 2 * K;           // 3072 soft bits per symbol
+constexpr int FRAME_SOFT = NSYM * SYMBITS;
+constexpr int INPUT_RATE = 2048000;
+
+// device tables for the OFDM kernels (built on the host with the reference's
+// own float expressions, see dabgpu.cpp: make_tables)
+struct OfdmTables {
+    const float2 *osc;      // oscillatorTable[2048000] (ofdm-processor.cpp:79-81)
+    const float2 *tw;       // twiddle bases [12][64]: rows a=0..7 W2048^{n2*a}, rows 8+b W2048^{n2*8b}
+    const float2 *ref_l;    // PRS refTable in FFT output lane layout [i][lane]
+    const uint32_t *cmap_l; // carrier of FFT bin, lane layout [i/2][lane], two int16 per word (-1 unused)
+    const float *refarg;    // refArg[18] (ofdm-decoder.cpp:71-74)
+};
+
+struct AcqJob {
+    int64_t iq_base;
+    int64_t start;
+    int64_t end;
+    int32_t local_phase;
+    int32_t phase;          // coarse + fine
+};
+struct AcqResult {
+    int64_t window;
+    int32_t local_phase;
+    int32_t status;
+    int32_t attempts;
+    int32_t pad;
+};
+
+// ---- Viterbi ------------------------------------------------------------
+constexpr int VCH = 48;                    // trellis steps per decision tile
+
+// depuncturing profile: up to 4 (L_i, PI_i) segments + the 24-bit PI_X tail
+// (deconvolve.cpp:172-237, fic-handler.cpp:254-288)
+struct Profile {
+    int32_t nbits;          // decoded bits N; trellis steps N+6
+    int32_t nseg;           // 0 = no puncturing (mother code given directly)
+    uint32_t mask[4];       // PI vectors as 32-bit masks (bit j = P_Code[j])
+    int32_t blk_end[4];     // cumulative 128-bit blocks at end of segment
+    int32_t in_base[5];     // input soft-bit index at segment start / tail start
+    uint32_t tail_mask;     // PI_X (24 bits)
+    int32_t frag;           // punctured input length (fragment size)
+};
+
+enum SrcKind : int32_t {
+    SRC_MOTHER = 0,         // contiguous depunctured stream, stride 4*(N+6)
+    SRC_FRAG = 1,           // contiguous punctured fragments, stride frag_stride
+    SRC_FIC = 2,            // FIC blocks inside the demod soft-bit buffer
+    SRC_MSC = 3,            // MSC subchannels with 16-CIF time de-interleave from the ring
+};
+
+struct VitJob {
+    int32_t kind;
+    int32_t n_cw;
+    const int16_t *src;
+    int64_t src_stride;     // SRC_MOTHER / SRC_FRAG: elements per codeword
+    const Profile *prof;    // per-profile table
+    const int32_t *cw_prof; // SRC_FRAG: profile per codeword; else null (profile 0 / by subch)
+    // SRC_FIC: codeword = 4*i + blk over slots[i]
+    const int32_t *slots;
+    // SRC_MSC: codeword = ((stream * ncif) + c) * nsub + sub
+    int32_t nsub, ncif, ring;      // subchannels, CIFs in this batch, ring frames
+    int64_t cif0;                   // global CIF index of the batch's first CIF (per stream, same for all)
+    int32_t first_slot;             // ring slot of the batch's first frame
+    const int16_t *sub_start;       // startAddr*64 per subchannel
+    // outputs
+    uint64_t *dec;                  // decision tiles
+    const int64_t *dec_off;         // per-codeword tile offset (u64 units); null: cw * tiles_max * VCH
+    int32_t tiles_max;
+    uint8_t *out;
+    int64_t out_stride;             // bytes per codeword
+    int32_t prbs;                   // xor energy-dispersal sequence
+    const uint32_t *prbs_words;     // PRBS packed 32 bits per word, bit i = prbs[32w+i]
+    const uint8_t *valid;           // optional per-codeword flag: 0 = skip
+};
+
+hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+                           int level, int32_t *si, float *mx, float *sm, bool general);
+hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+                         int16_t *corr, bool general);
+hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
+                        const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general);
+hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
+hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
+                          AcqResult *res);
+hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
+hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
+
+}  // namespace dab

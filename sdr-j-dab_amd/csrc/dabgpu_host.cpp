@@ -1,0 +1,980 @@
+// dabgpu_host.cpp -- the C ABI (include/dabgpu.h): context, device tables,
+// batched operators and the streaming pipeline that replaces
+// ofdmProcessor::run + ficHandler + mscHandler for many ensembles at once.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <cstdarg>
+#include <string>
+#include <vector>
+#include <mutex>
+#include <algorithm>
+#include "../../include/dabgpu.h"
+#include "dab_kernels.h"
+#include "dab_tables.h"
+
+using namespace dab;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+static int fail(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+#define HIPCHK(expr)                                                                               \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return fail(DABGPU_E_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), \
+                                          __FILE__, __LINE__);                                      \
+    } while (0)
+
+// ------------------------------------------------------------- host tables
+namespace {
+
+constexpr int M = 2048000;
+
+int brev5h(int k) { return ((k & 1) << 4) | ((k & 2) << 2) | (k & 4) | ((k & 8) >> 2) | ((k & 16) >> 4); }
+
+// Mode-I phase reference rows (k_min, i, n), k_max = k_min + 31 (phasetable.cpp:115-166)
+const int16_t kPhi[48][3] = {
+    {-768,0,1},{-736,1,2},{-704,2,0},{-672,3,1},{-640,0,3},{-608,1,2},{-576,2,2},{-544,3,3},
+    {-512,0,2},{-480,1,1},{-448,2,2},{-416,3,3},{-384,0,1},{-352,1,2},{-320,2,3},{-288,3,3},
+    {-256,0,2},{-224,1,2},{-192,2,2},{-160,3,1},{-128,0,1},{ -96,1,3},{ -64,2,1},{ -32,3,2},
+    {   1,0,3},{  33,3,1},{  65,2,1},{  97,1,1},{ 129,0,2},{ 161,3,2},{ 193,2,1},{ 225,1,0},
+    { 257,0,2},{ 289,3,2},{ 321,2,3},{ 353,1,3},{ 385,0,0},{ 417,3,2},{ 449,2,1},{ 481,1,3},
+    { 513,0,3},{ 545,3,3},{ 577,2,3},{ 609,1,0},{ 641,0,3},{ 673,3,0},{ 705,2,1},{ 737,1,1}};
+const int8_t kHpar[4][16] = {
+    {0,2,0,0,0,0,1,1,2,0,0,0,2,2,1,1},
+    {0,3,2,3,0,1,3,0,2,1,2,3,2,3,3,0},
+    {0,0,0,2,0,2,1,3,2,2,0,2,2,0,1,3},
+    {0,1,2,1,0,3,3,2,2,3,2,1,2,1,3,2}};
+
+float get_phi(int k) {                                   // phasetable.cpp:261-274 (float result)
+    for (auto &r : kPhi)
+        if (r[0] <= k && k <= r[0] + 31) return (float)(M_PI / 2 * (kHpar[r[1]][(k - r[0]) & 15] + r[2]));
+    return 0.0f;
+}
+
+struct HostTables {
+    std::vector<float2> osc, tw, ref_l;
+    std::vector<uint32_t> cmap_l, prbs_words;
+    std::vector<float> refarg;
+    std::vector<float2> ref;                // natural order refTable
+    std::vector<int16_t> perm;              // carrier -> signed carrier (mapIn)
+    HostTables() {
+#pragma clang fp contract(off)
+        osc.resize(M);
+        for (int i = 0; i < M; i++)          // ofdm-processor.cpp:79-81
+            osc[i] = make_float2((float)cos(2.0 * M_PI * i / M), (float)sin(2.0 * M_PI * i / M));
+        tw.resize(12 * 64);
+        for (int n2 = 0; n2 < 64; n2++) {
+            for (int a = 0; a < 8; a++) {
+                double ph = -2.0 * M_PI * (double)(n2 * a) / 2048.0;
+                tw[a * 64 + n2] = make_float2((float)cos(ph), (float)sin(ph));
+            }
+            for (int b = 0; b < 4; b++) {
+                double ph = -2.0 * M_PI * (double)(n2 * 8 * b) / 2048.0;
+                tw[(8 + b) * 64 + n2] = make_float2((float)cos(ph), (float)sin(ph));
+            }
+        }
+        ref.assign(2048, make_float2(0.0f, 0.0f));
+        for (int i = 1; i <= 768; i++) {      // phasereference.cpp:42-47
+            float phi = get_phi(i);
+            ref[i] = make_float2(cosf(phi), sinf(phi));
+            phi = get_phi(-i);
+            ref[2048 - i] = make_float2(cosf(phi), sinf(phi));
+        }
+        // mapper.cpp:33-55 (Mode I: V1 = 511, [256, 1792] \ {1024})
+        int16_t seq[2048];
+        seq[0] = 0;
+        for (int i = 1; i < 2048; i++) seq[i] = (int16_t)((13 * seq[i - 1] + 511) % 2048);
+        for (int i = 0; i < 2048; i++) {
+            int v = seq[i];
+            if (v == 1024 || v < 256 || v > 256 + 1536) continue;
+            perm.push_back((int16_t)(v - 1024));
+        }
+        std::vector<int> carrier_of_bin(2048, -1);
+        for (int c = 0; c < 1536; c++) { int k = perm[c]; carrier_of_bin[k < 0 ? k + 2048 : k] = c; }
+        ref_l.resize(32 * 64);
+        cmap_l.resize(16 * 64);
+        for (int lane = 0; lane < 64; lane++) {
+            int k1 = lane >> 1, r = lane & 1;
+            for (int i = 0; i < 32; i++) {
+                int bin = k1 + 32 * brev5h(i) + 1024 * r;
+                ref_l[i * 64 + lane] = ref[bin];
+                uint32_t c = (uint32_t)(uint16_t)(int16_t)carrier_of_bin[bin];
+                if (i & 1) cmap_l[(i >> 1) * 64 + lane] |= c << 16;
+                else cmap_l[(i >> 1) * 64 + lane] = c;
+            }
+        }
+        refarg.resize(18);
+        for (int i = 0; i < 18; i++) {        // ofdm-decoder.cpp:71-74
+            float2 a = ref[(2048 + i) % 2048], b = ref[(2048 + i + 1) % 2048];
+            float nb = -b.y;
+            float ac = a.x * b.x, bd = a.y * nb, ad = a.x * nb, bc = a.y * b.x;
+            float re = ac - bd, im = ad + bc;
+            refarg[i] = atan2f(im, re);
+        }
+        // energy dispersal (fic-handler.cpp:100-108), 32768 bits
+        prbs_words.assign(1024, 0u);
+        uint8_t sr[9];
+        memset(sr, 1, 9);
+        for (int i = 0; i < 32768; i++) {
+            uint8_t b = sr[8] ^ sr[4];
+            for (int j = 8; j > 0; j--) sr[j] = sr[j - 1];
+            sr[0] = b;
+            if (b) prbs_words[i >> 5] |= 1u << (i & 31);
+        }
+    }
+};
+const HostTables &host_tables() {
+    static HostTables t;
+    return t;
+}
+
+// depuncturing profile of a subchannel (deconvolve.cpp:142-366)
+int make_profile(const dabgpu_subch &s, Profile &p) {
+    memset(&p, 0, sizeof p);
+    int Ls[4] = {0, 0, 0, 0}, PIs[4] = {0, 0, 0, 0}, nseg = 0;
+    const int br = s.bitRate;
+    if (s.uepFlag == 0) {
+        int idx = -1;
+        for (int i = 0; i < kNumUep; i++)
+            if (kUepProfiles[i][0] == br && kUepProfiles[i][1] == s.protLevel) { idx = i; break; }
+        if (idx < 0) idx = 1;               // deconvolve.cpp:150-153 fallback
+        for (int j = 0; j < 4; j++) { Ls[j] = kUepProfiles[idx][2 + j]; PIs[j] = kUepProfiles[idx][6 + j]; }
+        nseg = 4;
+    } else {
+        const int lvl = s.protLevel & 7;
+        if (s.protLevel & 0100) {
+            switch (lvl) {
+            case 1: Ls[0] = 6 * br / 8 - 3; Ls[1] = 3; PIs[0] = 24; PIs[1] = 23; break;
+            case 2: if (br == 8) { Ls[0] = 5; Ls[1] = 1; PIs[0] = 13; PIs[1] = 12; }
+                    else { Ls[0] = 2 * br / 8 - 3; Ls[1] = 4 * br / 8 + 3; PIs[0] = 14; PIs[1] = 13; } break;
+            case 3: Ls[0] = 6 * br / 8 - 3; Ls[1] = 3; PIs[0] = 8; PIs[1] = 7; break;
+            case 4: Ls[0] = 4 * br / 8 - 3; Ls[1] = 2 * br / 8 + 3; PIs[0] = 3; PIs[1] = 2; break;
+            default: return -1;
+            }
+        } else if (s.protLevel & 0200) {
+            Ls[0] = 24 * br / 32 - 3; Ls[1] = 3;
+            switch (lvl) {
+            case 4: PIs[0] = 2; PIs[1] = 1; break;
+            case 3: PIs[0] = 4; PIs[1] = 3; break;
+            case 2: PIs[0] = 6; PIs[1] = 5; break;
+            case 1: PIs[0] = 10; PIs[1] = 9; break;
+            default: return -1;
+            }
+        } else {
+            return -1;                       // protection not defined by the reference
+        }
+        nseg = 2;
+    }
+    p.nbits = 24 * br;
+    // drop empty segments, keep order
+    int ns = 0, blk = 0, in = 0;
+    for (int j = 0; j < nseg; j++) {
+        if (Ls[j] <= 0) continue;
+        uint32_t m = pcode_mask(PIs[j]);
+        p.mask[ns] = m;
+        p.in_base[ns] = in;
+        blk += Ls[j];
+        in += Ls[j] * 4 * __builtin_popcount(m);
+        p.blk_end[ns] = blk;
+        ns++;
+    }
+    p.nseg = ns;
+    p.in_base[ns] = in;
+    p.tail_mask = kPiXMask;
+    p.frag = in + 12;
+    if (blk * 128 != 4 * p.nbits) return -2;  // profile inconsistent with bitRate
+    return 0;
+}
+
+Profile fic_profile() {                      // fic-handler.cpp:254-288
+    Profile p;
+    memset(&p, 0, sizeof p);
+    p.nbits = 768;
+    p.nseg = 2;
+    p.mask[0] = pcode_mask(16);
+    p.mask[1] = pcode_mask(15);
+    p.blk_end[0] = 21;
+    p.blk_end[1] = 24;
+    p.in_base[0] = 0;
+    p.in_base[1] = 21 * 4 * 24;
+    p.in_base[2] = p.in_base[1] + 3 * 4 * 23;
+    p.tail_mask = kPiXMask;
+    p.frag = 2304;
+    return p;
+}
+
+}  // namespace
+
+// ----------------------------------------------------------------- context
+struct dabgpu_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[16] = {};
+    float2 *osc = nullptr, *tw = nullptr, *ref_l = nullptr;
+    uint32_t *cmap_l = nullptr, *prbs = nullptr;
+    float *refarg = nullptr;
+    OfdmTables T{};
+    // growable scratch
+    void *scratch[8] = {};
+    size_t scratch_sz[8] = {};
+};
+
+static int scratch(dabgpu_ctx *c, int slot, size_t bytes, void **p) {
+    if (c->scratch_sz[slot] < bytes) {
+        if (c->scratch[slot]) HIPCHK(hipFree(c->scratch[slot]));
+        c->scratch[slot] = nullptr;
+        c->scratch_sz[slot] = 0;
+        size_t sz = std::max<size_t>(bytes, 4096);
+        HIPCHK(hipMalloc(&c->scratch[slot], sz));
+        c->scratch_sz[slot] = sz;
+    }
+    *p = c->scratch[slot];
+    return 0;
+}
+enum { SC_DEC = 0, SC_PROF = 1, SC_I32 = 2, SC_FRAMES = 3, SC_FC = 4, SC_MISC = 5 };
+
+template <class T>
+static int upload(dabgpu_ctx *c, T **dst, const std::vector<T> &v) {
+    HIPCHK(hipMalloc((void **)dst, v.size() * sizeof(T)));
+    HIPCHK(hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+    return 0;
+}
+
+extern "C" {
+
+int dabgpu_abi_version(void) { return DABGPU_ABI_VERSION; }
+const char *dabgpu_last_error(void) { return g_err.c_str(); }
+
+int dabgpu_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
+    if (!out) return fail(DABGPU_E_ARG, "out is null");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(DABGPU_E_NODEV, "no HIP device");
+    if (device < 0 || device >= n) return fail(DABGPU_E_ARG, "device %d out of range (%d)", device, n);
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(DABGPU_E_NODEV, "device %d is %s, this build targets gfx950", device, prop.gcnArchName);
+    HIPCHK(hipSetDevice(device));
+    auto *c = new dabgpu_ctx();
+    c->device = device;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
+    const HostTables &t = host_tables();
+    int rc = 0;
+    if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->tw, t.tw)) || (rc = upload(c, &c->ref_l, t.ref_l)) ||
+        (rc = upload(c, &c->cmap_l, t.cmap_l)) || (rc = upload(c, &c->prbs, t.prbs_words)) ||
+        (rc = upload(c, &c->refarg, t.refarg))) {
+        dabgpu_ctx_destroy(c);
+        return rc;
+    }
+    c->T.osc = c->osc;
+    c->T.tw = c->tw;
+    c->T.ref_l = c->ref_l;
+    c->T.cmap_l = c->cmap_l;
+    c->T.refarg = c->refarg;
+    *out = c;
+    return 0;
+}
+
+int dabgpu_ctx_destroy(dabgpu_ctx *c) {
+    if (!c) return 0;
+    (void)hipSetDevice(c->device);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->cmap_l, (void *)c->prbs,
+                    (void *)c->refarg})
+        if (p) (void)hipFree(p);
+    for (auto p : c->scratch) if (p) (void)hipFree(p);
+    for (auto e : c->ev) if (e) (void)hipEventDestroy(e);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
+    delete c;
+    return 0;
+}
+
+int dabgpu_sync(dabgpu_ctx *c) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+int dabgpu_alloc(dabgpu_ctx *c, size_t bytes, void **p) {
+    if (!c || !p) return fail(DABGPU_E_ARG, "null arg");
+    HIPCHK(hipSetDevice(c->device));
+    if (hipMalloc(p, bytes) != hipSuccess) return fail(DABGPU_E_NOMEM, "hipMalloc(%zu) failed", bytes);
+    return 0;
+}
+int dabgpu_free(dabgpu_ctx *c, void *p) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    if (p) HIPCHK(hipFree(p));
+    return 0;
+}
+int dabgpu_memcpy_h2d(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+int dabgpu_memcpy_d2h(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+int dabgpu_memset_d(dabgpu_ctx *c, void *dst, int value, size_t bytes) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    HIPCHK(hipMemsetAsync(dst, value, bytes, c->stream));
+    return 0;
+}
+int dabgpu_event_record(dabgpu_ctx *c, int slot) {
+    if (!c || slot < 0 || slot >= 16) return fail(DABGPU_E_ARG, "bad event slot");
+    HIPCHK(hipEventRecord(c->ev[slot], c->stream));
+    return 0;
+}
+int dabgpu_event_elapsed(dabgpu_ctx *c, int a, int b, float *ms) {
+    if (!c || a < 0 || a >= 16 || b < 0 || b >= 16 || !ms) return fail(DABGPU_E_ARG, "bad event slot");
+    HIPCHK(hipEventSynchronize(c->ev[b]));
+    HIPCHK(hipEventElapsedTime(ms, c->ev[a], c->ev[b]));
+    return 0;
+}
+
+// ---- OFDM operators --------------------------------------------------------
+int dabgpu_prs_sync(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t level, int32_t *si,
+                    float *mx, float *sm) {
+    if (!c || !iq || !fr || !si || n < 0) return fail(DABGPU_E_ARG, "bad args");
+    HIPCHK(launch_prs_sync(c->stream, iq, fr, n, c->T, level, si, mx, sm, true));
+    return 0;
+}
+int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t *corr) {
+    if (!c || !iq || !fr || !corr || n < 0) return fail(DABGPU_E_ARG, "bad args");
+    HIPCHK(launch_block0(c->stream, iq, fr, n, c->T, corr, true));
+    return 0;
+}
+static const int kChunks = 3;
+static int demod_impl(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t *soft, float *softf,
+                      float *fc, bool general) {
+    void *part = nullptr;
+    int rc = scratch(c, SC_FC, sizeof(float2) * (size_t)n * kChunks, &part);
+    if (rc) return rc;
+    HIPCHK(launch_demod(c->stream, iq, fr, n, kChunks, c->T, soft, softf, (float *)part, general));
+    if (fc) HIPCHK(launch_fc_reduce(c->stream, (const float *)part, kChunks, n, fc));
+    return 0;
+}
+int dabgpu_ofdm_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t *soft, float *softf,
+                      float *fc) {
+    if (!c || !iq || !fr || !soft || n < 0) return fail(DABGPU_E_ARG, "bad args");
+    return demod_impl(c, iq, fr, n, soft, softf, fc, true);
+}
+
+// ---- Viterbi operators -------------------------------------------------------
+static int run_viterbi(dabgpu_ctx *c, VitJob &J, int max_nbits) {
+    const int tiles = (max_nbits + 6 + VCH - 1) / VCH;
+    void *dec = nullptr;
+    int rc = scratch(c, SC_DEC, sizeof(uint64_t) * (size_t)J.n_cw * tiles * VCH, &dec);
+    if (rc) return rc;
+    J.dec = (uint64_t *)dec;
+    J.tiles_max = tiles;
+    J.prbs_words = c->prbs;
+    HIPCHK(launch_viterbi(c->stream, J));
+    return 0;
+}
+
+int dabgpu_viterbi(dabgpu_ctx *c, const int16_t *in, int n_cw, int nbits, uint8_t *out) {
+    if (!c || !in || !out || n_cw < 0 || nbits <= 0 || nbits > 32768) return fail(DABGPU_E_ARG, "bad args");
+    Profile p;
+    memset(&p, 0, sizeof p);
+    p.nbits = nbits;
+    void *pd = nullptr;
+    int rc = scratch(c, SC_PROF, sizeof p, &pd);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(pd, &p, sizeof p, hipMemcpyHostToDevice, c->stream));
+    VitJob J;
+    memset(&J, 0, sizeof J);
+    J.kind = SRC_MOTHER;
+    J.n_cw = n_cw;
+    J.src = in;
+    J.src_stride = 4 * (int64_t)(nbits + 6);
+    J.prof = (const Profile *)pd;
+    J.out = out;
+    J.out_stride = nbits;
+    J.prbs = 0;
+    return run_viterbi(c, J, nbits);
+}
+
+static int fic_common(dabgpu_ctx *c, VitJob &J, uint8_t *bits, uint8_t *ok) {
+    Profile p = fic_profile();
+    void *pd = nullptr;
+    int rc = scratch(c, SC_PROF, sizeof p, &pd);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(pd, &p, sizeof p, hipMemcpyHostToDevice, c->stream));
+    J.prof = (const Profile *)pd;
+    J.out = bits;
+    J.out_stride = 768;
+    J.prbs = 1;
+    if ((rc = run_viterbi(c, J, 768))) return rc;
+    if (ok) HIPCHK(launch_fic_post(c->stream, bits, ok, 3 * J.n_cw));
+    return 0;
+}
+
+int dabgpu_fic_decode(dabgpu_ctx *c, const int16_t *soft, int n, uint8_t *bits, uint8_t *ok) {
+    if (!c || !soft || !bits || n < 0) return fail(DABGPU_E_ARG, "bad args");
+    VitJob J;
+    memset(&J, 0, sizeof J);
+    J.kind = SRC_FRAG;
+    J.n_cw = n;
+    J.src = soft;
+    J.src_stride = 2304;
+    return fic_common(c, J, bits, ok);
+}
+
+int dabgpu_fic_decode_frames(dabgpu_ctx *c, const int16_t *soft, const int32_t *slots_h, int nf, uint8_t *bits,
+                             uint8_t *ok) {
+    if (!c || !soft || !slots_h || !bits || nf < 0) return fail(DABGPU_E_ARG, "bad args");
+    void *sd = nullptr;
+    int rc = scratch(c, SC_I32, sizeof(int32_t) * (size_t)std::max(nf, 1), &sd);
+    if (rc) return rc;
+    HIPCHK(hipMemcpyAsync(sd, slots_h, sizeof(int32_t) * nf, hipMemcpyHostToDevice, c->stream));
+    VitJob J;
+    memset(&J, 0, sizeof J);
+    J.kind = SRC_FIC;
+    J.n_cw = 4 * nf;
+    J.src = soft;
+    J.slots = (const int32_t *)sd;
+    rc = fic_common(c, J, bits, ok);
+    if (rc) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));       // slots scratch may be reused by the next call
+    return 0;
+}
+
+int dabgpu_msc_deconvolve(dabgpu_ctx *c, const int16_t *frag, int64_t frag_stride, const dabgpu_subch *sub,
+                          int n_cw, uint8_t *bits, int64_t out_stride) {
+    if (!c || !frag || !sub || !bits || n_cw < 0) return fail(DABGPU_E_ARG, "bad args");
+    std::vector<Profile> profs;
+    std::vector<int32_t> cwp(n_cw);
+    int maxbits = 8;
+    for (int i = 0; i < n_cw; i++) {
+        Profile p;
+        int rc = make_profile(sub[i], p);
+        if (rc) return fail(DABGPU_E_UNSUP, "subchannel %d: protection (uep=%d, level 0%o, %d kbps) undefined",
+                            i, sub[i].uepFlag, sub[i].protLevel, sub[i].bitRate);
+        if (p.frag > frag_stride) return fail(DABGPU_E_ARG, "fragment stride %lld < %d", (long long)frag_stride, p.frag);
+        if (p.nbits > out_stride) return fail(DABGPU_E_ARG, "out stride too small");
+        int found = -1;
+        for (size_t j = 0; j < profs.size(); j++)
+            if (!memcmp(&profs[j], &p, sizeof p)) { found = (int)j; break; }
+        if (found < 0) { found = (int)profs.size(); profs.push_back(p); }
+        cwp[i] = found;
+        maxbits = std::max(maxbits, p.nbits);
+    }
+    void *pd = nullptr, *cd = nullptr;
+    int rc = scratch(c, SC_PROF, sizeof(Profile) * std::max<size_t>(profs.size(), 1), &pd);
+    if (rc) return rc;
+    if ((rc = scratch(c, SC_I32, sizeof(int32_t) * std::max(n_cw, 1), &cd))) return rc;
+    if (!profs.empty()) HIPCHK(hipMemcpyAsync(pd, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice, c->stream));
+    if (n_cw) HIPCHK(hipMemcpyAsync(cd, cwp.data(), sizeof(int32_t) * n_cw, hipMemcpyHostToDevice, c->stream));
+    VitJob J;
+    memset(&J, 0, sizeof J);
+    J.kind = SRC_FRAG;
+    J.n_cw = n_cw;
+    J.src = frag;
+    J.src_stride = frag_stride;
+    J.prof = (const Profile *)pd;
+    J.cw_prof = (const int32_t *)cd;
+    J.out = bits;
+    J.out_stride = out_stride;
+    J.prbs = 1;
+    if ((rc = run_viterbi(c, J, maxbits))) return rc;
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
+}  // extern "C"
+
+// ========================================================================
+// streaming pipeline
+// ========================================================================
+struct StreamSt {
+    int64_t window = 0;      // next SyncOnPhase position
+    int32_t lp = 0;          // localPhase before `window`
+    int32_t coarse = 0;
+    int16_t fine = 0;
+    bool f2 = true;
+    int16_t prev1 = 1000, prev2 = 999;
+    bool synced = false;
+    int64_t cif_count = 0;
+    int64_t frame_count = 0;
+    int32_t last_si = 504;
+    int32_t resyncs = 0;
+};
+
+struct dabgpu_pipe {
+    dabgpu_ctx *c = nullptr;
+    int S = 0, F = 0, NSUB = 0, R = 0;
+    int16_t threshold = 3;
+    std::vector<dabgpu_subch> sub;
+    std::vector<StreamSt> st;
+    int16_t *ring = nullptr;         // [S][R][75][3072]
+    Profile *prof_d = nullptr;       // [NSUB]
+    int16_t *substart_d = nullptr;   // [NSUB]
+    dabgpu_frame *frames_d = nullptr;
+    int32_t *si_d = nullptr;
+    int16_t *corr_d = nullptr;
+    float *fc_d = nullptr, *fcpart_d = nullptr;
+    int32_t *slots_d = nullptr;
+    uint64_t *dec_d = nullptr;
+    size_t dec_sz = 0;
+    int max_nbits = 0;
+    std::vector<dabgpu_frame> last_frames;   // [S][F]
+    std::vector<int32_t> last_si;
+};
+
+namespace {
+inline int32_t modM(int64_t x) {
+    int64_t r = x % M;
+    return (int32_t)(r < 0 ? r + M : r);
+}
+// advance localPhase over n samples read with `phase` (getSamples, ofdm-processor.cpp:217-219)
+inline int32_t lp_after(int32_t lp, int64_t n, int32_t phase) { return modM((int64_t)lp - n * (int64_t)phase); }
+}  // namespace
+
+extern "C" {
+
+int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **out) {
+    if (!c || !cfg || !out) return fail(DABGPU_E_ARG, "null arg");
+    *out = nullptr;
+    if (cfg->n_streams <= 0 || cfg->n_frames <= 0 || cfg->n_subch < 0) return fail(DABGPU_E_ARG, "bad sizes");
+    if (cfg->freq_sync_method != 1) return fail(DABGPU_E_UNSUP, "freqSyncMethod %d not implemented (only 1)", cfg->freq_sync_method);
+    auto *p = new dabgpu_pipe();
+    p->c = c;
+    p->S = cfg->n_streams;
+    p->F = cfg->n_frames;
+    p->NSUB = cfg->n_subch;
+    p->R = cfg->n_frames + 4;
+    p->threshold = cfg->threshold;
+    p->sub.assign(cfg->subch, cfg->subch + cfg->n_subch);
+    p->st.assign(p->S, StreamSt());
+    std::vector<Profile> profs(std::max(1, p->NSUB));
+    std::vector<int16_t> ss(std::max(1, p->NSUB), 0);
+    p->max_nbits = 768;
+    for (int i = 0; i < p->NSUB; i++) {
+        if (make_profile(p->sub[i], profs[i])) {
+            delete p;
+            return fail(DABGPU_E_UNSUP, "subchannel %d protection undefined", i);
+        }
+        if (p->sub[i].startAddr < 0 || p->sub[i].startAddr + p->sub[i].length > 864 || profs[i].frag > p->sub[i].length * 64) {
+            delete p;
+            return fail(DABGPU_E_ARG, "subchannel %d does not fit its CUs", i);
+        }
+        ss[i] = (int16_t)(p->sub[i].startAddr * 64);
+        p->max_nbits = std::max(p->max_nbits, profs[i].nbits);
+    }
+    const size_t SF = (size_t)p->S * p->F;
+    int rc = 0;
+    auto A = [&](void **ptr, size_t bytes) {
+        if (rc) return;
+        if (hipMalloc(ptr, std::max<size_t>(bytes, 256)) != hipSuccess) rc = fail(DABGPU_E_NOMEM, "pipe alloc %zu", bytes);
+    };
+    A((void **)&p->ring, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT);
+    A((void **)&p->prof_d, sizeof(Profile) * profs.size());
+    A((void **)&p->substart_d, sizeof(int16_t) * ss.size());
+    A((void **)&p->frames_d, sizeof(dabgpu_frame) * SF);
+    A((void **)&p->si_d, sizeof(int32_t) * SF);
+    A((void **)&p->corr_d, sizeof(int16_t) * SF);
+    A((void **)&p->fc_d, sizeof(float2) * SF);
+    A((void **)&p->fcpart_d, sizeof(float2) * SF * kChunks);
+    A((void **)&p->slots_d, sizeof(int32_t) * SF);
+    const int tiles = (p->max_nbits + 6 + VCH - 1) / VCH;
+    const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
+    p->dec_sz = sizeof(uint64_t) * ncw * tiles * VCH;
+    A((void **)&p->dec_d, p->dec_sz);
+    if (!rc) {
+        if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(p->substart_d, ss.data(), sizeof(int16_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemset(p->ring, 0, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
+            rc = fail(DABGPU_E_HIP, "pipe init copy failed");
+    }
+    if (rc) {
+        dabgpu_pipe_destroy(p);
+        return rc;
+    }
+    *out = p;
+    return 0;
+}
+
+int dabgpu_pipe_destroy(dabgpu_pipe *p) {
+    if (!p) return 0;
+    (void)hipStreamSynchronize(p->c->stream);
+    for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
+                    (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d})
+        if (x) (void)hipFree(x);
+    delete p;
+    return 0;
+}
+
+int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *start_h, const int64_t *n_avail_h) {
+    if (!p || !iq || !start_h || !n_avail_h) return fail(DABGPU_E_ARG, "null arg");
+    dabgpu_ctx *c = p->c;
+    std::vector<AcqJob> jobs;
+    std::vector<int> who;
+    for (int s = 0; s < p->S; s++) {
+        if (p->st[s].synced) continue;
+        AcqJob j;
+        j.iq_base = stride * s;
+        j.start = start_h[s];
+        j.end = n_avail_h[s];
+        j.local_phase = p->st[s].lp;
+        j.phase = p->st[s].coarse + p->st[s].fine;
+        jobs.push_back(j);
+        who.push_back(s);
+    }
+    if (jobs.empty()) return 0;
+    void *jd = nullptr, *rd = nullptr;
+    int rc = scratch(c, SC_MISC, sizeof(AcqJob) * jobs.size(), &jd);
+    if (rc) return rc;
+    if ((rc = scratch(c, SC_FC, sizeof(AcqResult) * jobs.size(), &rd))) return rc;
+    HIPCHK(hipMemcpyAsync(jd, jobs.data(), sizeof(AcqJob) * jobs.size(), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_acquire(c->stream, iq, (const AcqJob *)jd, (int)jobs.size(), c->osc, (AcqResult *)rd));
+    std::vector<AcqResult> res(jobs.size());
+    HIPCHK(hipMemcpyAsync(res.data(), rd, sizeof(AcqResult) * jobs.size(), hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    int bad = 0;
+    for (size_t i = 0; i < jobs.size(); i++) {
+        StreamSt &S = p->st[who[i]];
+        S.lp = res[i].local_phase;
+        S.window = res[i].window;
+        if (res[i].status == 0) S.synced = true;
+        else bad++;
+    }
+    if (bad) return fail(DABGPU_E_STATE, "%d stream(s) found no null symbol", bad);
+    return 0;
+}
+
+// One speculative front-end pass over the uncommitted frames of every stream.
+// Predicts windows (startIndex = last one) and correctors (unchanged), runs the
+// batched kernels, then replays ofdmProcessor::run's sequential logic on the
+// host with the measured values and commits the longest correctly predicted
+// prefix of each stream (ofdm-processor.cpp:344-468).
+static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
+                           std::vector<int> &done, std::vector<StreamSt> &cur, bool &progress, bool &lost) {
+    dabgpu_ctx *c = p->c;
+    const int S = p->S, F = p->F;
+    std::vector<dabgpu_frame> fr;
+    std::vector<int> fs, ff;          // stream, frame of each pending entry
+    std::vector<int16_t> pred_f2;
+    std::vector<int32_t> pred_si;
+    bool general = false;
+    for (int s = 0; s < S; s++) {
+        if (done[s] >= F || !cur[s].synced) continue;
+        StreamSt x = cur[s];
+        for (int f = done[s]; f < F; f++) {
+            dabgpu_frame d;
+            memset(&d, 0, sizeof d);
+            const int32_t si = x.last_si;
+            const int32_t pa = x.coarse + x.fine;
+            d.iq_base = stride * s;
+            d.window = x.window;
+            d.block0 = x.window + si;
+            d.lp_window = x.lp;
+            d.phase_a = pa;
+            int64_t end = d.block0 + TU + (int64_t)NSYM * TS + TNULL;
+            if (end > n_avail[s]) break;                       // not enough samples for this frame
+            // f2 logic with the predicted correction 0 (ofdm-processor.cpp:395-406)
+            d.flags = x.f2 ? 1 : 0;
+            bool f2 = x.f2;
+            int16_t p1 = x.prev1, p2 = x.prev2;
+            if (f2) {
+                if (p1 == 0 && p2 == 0) f2 = false;
+                else { p2 = p1; p1 = 0; }
+            }
+            const int32_t pb = x.coarse + x.fine;
+            d.lp_data = lp_after(x.lp, (int64_t)TU + si, pa);
+            d.phase_b = pb;
+            d.out_slot = (int32_t)((int64_t)s * p->R + (x.frame_count + (f - done[s])) % p->R);
+            fr.push_back(d);
+            fs.push_back(s);
+            ff.push_back(f);
+            pred_si.push_back(si);
+            if (pa || pb) general = true;
+            // next frame prediction: fine unchanged, null skipped
+            int32_t lp_end = lp_after(d.lp_data, (int64_t)NSYM * TS, pb);
+            x.lp = lp_after(lp_end, TNULL, pb);
+            x.window = end;
+            x.f2 = f2; x.prev1 = p1; x.prev2 = p2;
+        }
+    }
+    const int n = (int)fr.size();
+    progress = false;
+    if (n == 0) return 0;
+    HIPCHK(hipMemcpyAsync(p->frames_d, fr.data(), sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
+    std::vector<int32_t> si(n);
+    HIPCHK(hipMemcpyAsync(si.data(), p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    // pass 1: windows.  A frame is usable if every earlier frame of its stream
+    // had the predicted startIndex; its own startIndex fixes block0.
+    std::vector<char> ok(n, 0);
+    std::vector<char> cut(n, 0);          // frames after this one are invalid
+    {
+        int prev_s = -1;
+        bool valid = true;
+        for (int i = 0; i < n; i++) {
+            if (fs[i] != prev_s) { prev_s = fs[i]; valid = true; }
+            if (!valid) continue;
+            if (si[i] < 0) {               // sync lost (ofdm-processor.cpp:354-357)
+                valid = false;
+                continue;
+            }
+            ok[i] = 1;
+            fr[i].block0 = fr[i].window + si[i];
+            fr[i].lp_data = lp_after(fr[i].lp_window, (int64_t)TU + si[i], fr[i].phase_a);
+            if (si[i] != pred_si[i]) { cut[i] = 1; valid = false; }
+        }
+    }
+    // pass 2: block 0 (coarse AFC) for the usable frames with f2 on
+    std::vector<int> idx;
+    for (int i = 0; i < n; i++) if (ok[i]) idx.push_back(i);
+    std::vector<dabgpu_frame> fr2;
+    for (int i : idx) fr2.push_back(fr[i]);
+    const int n2 = (int)fr2.size();
+    std::vector<int16_t> corr(n2, 0);
+    bool any_f2 = false;
+    for (auto &d : fr2) if (d.flags & 1) any_f2 = true;
+    if (n2 && any_f2) {
+        HIPCHK(hipMemcpyAsync(p->frames_d, fr2.data(), sizeof(dabgpu_frame) * n2, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(launch_block0(c->stream, iq, p->frames_d, n2, c->T, p->corr_d, general));
+        HIPCHK(hipMemcpyAsync(corr.data(), p->corr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    // replay the coarse corrector with the measured corrections; phase_b of a
+    // frame uses its own correction, later frames are cut if the corrector moved
+    {
+        int prev_s = -1;
+        StreamSt x;
+        bool valid = true;
+        for (int k = 0; k < n2; k++) {
+            const int i = idx[k];
+            if (fs[i] != prev_s) { prev_s = fs[i]; x = cur[fs[i]]; valid = true; }
+            if (!valid) { ok[i] = 0; continue; }
+            const int32_t coarse0 = x.coarse;
+            if (x.f2) {
+                const int16_t cr = corr[k];
+                if (cr == 0 && x.prev1 == 0 && x.prev2 == 0) x.f2 = false;
+                else if (cr != 100) {
+                    x.coarse += cr * 1000;
+                    if (std::abs(x.coarse) > 35000) x.coarse = 0;
+                    x.prev2 = x.prev1;
+                    x.prev1 = cr;
+                }
+            }
+            fr2[k].phase_b = x.coarse + x.fine;
+            fr[i].phase_b = fr2[k].phase_b;
+            if (fr2[k].phase_b) general = true;
+            if (corr[k] != 0 || x.coarse != coarse0) cut[i] = 1;   // prediction assumed correction 0
+            if (cut[i]) valid = false;
+        }
+    }
+    std::vector<int16_t> corr_i(n, 0);
+    for (int k = 0; k < n2; k++) corr_i[idx[k]] = corr[k];
+    // pass 3: demod of the frames still usable
+    std::vector<int> idx3;
+    std::vector<dabgpu_frame> fr3;
+    for (int k = 0; k < n2; k++) if (ok[idx[k]]) { idx3.push_back(idx[k]); fr3.push_back(fr2[k]); }
+    const int n3 = (int)fr3.size();
+    std::vector<float2> fc(n3);
+    if (n3) {
+        HIPCHK(hipMemcpyAsync(p->frames_d, fr3.data(), sizeof(dabgpu_frame) * n3, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general));
+        HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
+        HIPCHK(hipMemcpyAsync(fc.data(), p->fc_d, sizeof(float2) * n3, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipStreamSynchronize(c->stream));
+    }
+    // commit: replay the full per-frame state update (ofdm-processor.cpp:395-468)
+    {
+        int prev_s = -1;
+        bool valid = true;
+        for (int k = 0; k < n3; k++) {
+            const int i = idx3[k];
+            const int s = fs[i];
+            if (s != prev_s) { prev_s = s; valid = true; }
+            if (!valid) continue;
+            StreamSt &x = cur[s];
+            const dabgpu_frame &d = fr3[k];
+            // coarse (same replay as above)
+            if (x.f2) {
+                const int16_t cr = corr_i[i];
+                if (cr == 0 && x.prev1 == 0 && x.prev2 == 0) x.f2 = false;
+                else if (cr != 100) {
+                    x.coarse += cr * 1000;
+                    if (std::abs(x.coarse) > 35000) x.coarse = 0;
+                    x.prev2 = x.prev1;
+                    x.prev1 = cr;
+                }
+            }
+            const int16_t fine0 = x.fine;
+            const int32_t coarse0 = x.coarse;
+            // fineCorrector += 0.1 * arg(FreqCorr) / M_PI * (carrierDiff / 2)
+            const float a = atan2f(fc[k].y, fc[k].x);
+            x.fine = (int16_t)(x.fine + 0.1 * a / M_PI * (1000 / 2));
+            int32_t lp_end = lp_after(d.lp_data, (int64_t)NSYM * TS, d.phase_b);
+            x.lp = lp_after(lp_end, TNULL, x.coarse + x.fine);
+            if (x.fine > 500) { x.coarse += 1000; x.fine -= 1000; }
+            else if (x.fine < -500) { x.coarse -= 1000; x.fine += 1000; }
+            x.window = d.block0 + TU + (int64_t)NSYM * TS + TNULL;
+            x.last_si = (int32_t)(d.block0 - d.window);
+            p->last_frames[(size_t)s * p->F + done[s]] = d;
+            p->last_si[(size_t)s * p->F + done[s]] = x.last_si;
+            done[s]++;
+            x.frame_count++;
+            progress = true;
+            if (x.fine != fine0 || x.coarse != coarse0 || cut[i]) valid = false;
+        }
+    }
+    // sync loss: the first uncommitted frame's window was read exactly as the
+    // reference would and findIndex failed -> goto notSynced (ofdm-processor.cpp:354-357)
+    for (int i = 0; i < n; i++) {
+        const int s = fs[i];
+        StreamSt &x = cur[s];
+        if (ff[i] == done[s] && si[i] < 0 && fr[i].window == x.window && fr[i].lp_window == x.lp &&
+            fr[i].phase_a == x.coarse + x.fine) {
+            x.synced = false;
+            x.lp = lp_after(x.lp, TU, x.coarse + x.fine);
+            x.window += TU;
+            x.resyncs++;
+            lost = true;
+        }
+    }
+    return 0;
+}
+
+int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail, uint8_t *fic_bits,
+                    uint8_t *fic_crc, uint8_t *msc_bits, int32_t msc_stride, uint8_t *msc_valid) {
+    if (!p || !iq || !n_avail) return fail(DABGPU_E_ARG, "null arg");
+    dabgpu_ctx *c = p->c;
+    const int S = p->S, F = p->F;
+    for (int s = 0; s < S; s++) if (!p->st[s].synced) return fail(DABGPU_E_STATE, "stream %d not synchronised", s);
+    p->last_frames.assign((size_t)S * F, dabgpu_frame());
+    p->last_si.assign((size_t)S * F, 0);
+    std::vector<int> done(S, 0);
+    std::vector<StreamSt> cur = p->st;
+    bool lost = false;
+    for (int it = 0; it < 4 * F + 8; it++) {
+        bool progress = false;
+        int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost);
+        if (rc) return rc;
+        if (!progress) break;
+    }
+    bool all = true;
+    for (int s = 0; s < S; s++) if (done[s] != F) all = false;
+    // FIC for every committed frame
+    {
+        std::vector<int32_t> slots((size_t)S * F);
+        for (int s = 0; s < S; s++)
+            for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = p->last_frames[(size_t)s * F + f].out_slot;
+        if (fic_bits) {
+            HIPCHK(hipMemcpyAsync(p->slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, c->stream));
+            Profile pf = fic_profile();
+            void *pd = nullptr;
+            int rc = scratch(c, SC_PROF, sizeof pf, &pd);
+            if (rc) return rc;
+            HIPCHK(hipMemcpyAsync(pd, &pf, sizeof pf, hipMemcpyHostToDevice, c->stream));
+            VitJob J;
+            memset(&J, 0, sizeof J);
+            J.kind = SRC_FIC;
+            J.n_cw = 4 * S * F;
+            J.src = p->ring;
+            J.slots = p->slots_d;
+            J.prof = (const Profile *)pd;
+            J.out = fic_bits;
+            J.out_stride = 768;
+            J.prbs = 1;
+            J.prbs_words = c->prbs;
+            J.dec = p->dec_d;
+            J.tiles_max = (768 + 6 + VCH - 1) / VCH;
+            HIPCHK(launch_viterbi(c->stream, J));
+            if (fic_crc) HIPCHK(launch_fic_post(c->stream, fic_bits, fic_crc, 12 * S * F));
+        }
+    }
+    // MSC: all subchannels of all CIFs of this run
+    const int64_t cif0 = p->st[0].cif_count;
+    if (msc_bits && p->NSUB > 0 && all) {
+        if (msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
+        VitJob J;
+        memset(&J, 0, sizeof J);
+        J.kind = SRC_MSC;
+        J.n_cw = S * 4 * F * p->NSUB;
+        J.src = p->ring;
+        J.prof = p->prof_d;
+        J.nsub = p->NSUB;
+        J.ncif = 4 * F;
+        J.ring = p->R;
+        J.cif0 = cif0;
+        J.sub_start = p->substart_d;
+        J.out = msc_bits;
+        J.out_stride = msc_stride;
+        J.prbs = 1;
+        J.prbs_words = c->prbs;
+        J.dec = p->dec_d;
+        J.tiles_max = (p->max_nbits + 6 + VCH - 1) / VCH;
+        HIPCHK(launch_viterbi(c->stream, J));
+    }
+    if (msc_valid)
+        for (int s = 0; s < S; s++)
+            for (int q = 0; q < 4 * F; q++) msc_valid[(size_t)s * 4 * F + q] = (all && cif0 + q >= 16) ? 1 : 0;
+    for (int s = 0; s < S; s++) {
+        cur[s].cif_count = p->st[s].cif_count + 4 * (int64_t)done[s];
+    }
+    p->st = cur;
+    if (lost || !all) return fail(DABGPU_E_STATE, "a stream lost sync or ran out of samples (see dabgpu_pipe_state)");
+    return 0;
+}
+
+int dabgpu_pipe_state(dabgpu_pipe *p, int s, dabgpu_stream_state *o) {
+    if (!p || !o || s < 0 || s >= p->S) return fail(DABGPU_E_ARG, "bad args");
+    const StreamSt &x = p->st[s];
+    o->next_pos = x.window;
+    o->local_phase = x.lp;
+    o->coarse = x.coarse;
+    o->fine = x.fine;
+    o->f2correction = x.f2;
+    o->prev1 = x.prev1;
+    o->prev2 = x.prev2;
+    o->synced = x.synced;
+    o->cif_count = x.cif_count;
+    o->last_start_index = x.last_si;
+    o->resyncs = x.resyncs;
+    return 0;
+}
+
+int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft, int32_t *ring) {
+    if (!p || !soft || !ring) return fail(DABGPU_E_ARG, "bad args");
+    *soft = p->ring;
+    *ring = p->R;
+    return 0;
+}
+int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot) {
+    if (!p || !slot || frame < 0 || frame >= p->F) return fail(DABGPU_E_ARG, "bad args");
+    *slot = p->last_frames.empty() ? -1 : p->last_frames[frame].out_slot;
+    return 0;
+}
+int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *fr, int32_t *si) {
+    if (!p) return fail(DABGPU_E_ARG, "bad args");
+    if (fr) memcpy(fr, p->last_frames.data(), sizeof(dabgpu_frame) * p->last_frames.size());
+    if (si) memcpy(si, p->last_si.data(), sizeof(int32_t) * p->last_si.size());
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,317 @@
+"""dabamd -- Python mirror of the MI355X DAB Mode-I path (include/dabgpu.h).
+
+Thin ctypes layer over lib/libdabgpu.so.  The functions mirror the
+sdr-j-dab interfaces they replace (names and argument meaning follow the
+reference; file:line in each docstring).  There is no CPU fallback: if the
+HIP library or a gfx950 device is missing, every call raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_PKG = os.path.dirname(_HERE)
+LIB_PATH = os.path.join(_PKG, "lib", "libdabgpu.so")
+SYNTH_PATH = os.path.join(_PKG, "lib", "libdabsynth.so")
+
+TU, TS, TG, TNULL, TF, K, L = 2048, 2552, 504, 2656, 196608, 1536, 76
+NSYM = 75
+SYMBITS = 2 * K
+CIF_BITS = 55296
+
+
+class DabError(RuntimeError):
+    pass
+
+
+class Subch(C.Structure):
+    """audiodata/packetdata subset (dab-constants.h:151-176)."""
+    _fields_ = [("startAddr", C.c_int16), ("length", C.c_int16), ("bitRate", C.c_int16),
+                ("protLevel", C.c_int16), ("uepFlag", C.c_int16), ("reserved", C.c_int16)]
+
+
+class Frame(C.Structure):
+    _fields_ = [("iq_base", C.c_int64), ("window", C.c_int64), ("block0", C.c_int64),
+                ("lp_window", C.c_int32), ("phase_a", C.c_int32), ("lp_data", C.c_int32),
+                ("phase_b", C.c_int32), ("out_slot", C.c_int32), ("flags", C.c_int32)]
+
+
+class PipeCfg(C.Structure):
+    _fields_ = [("n_streams", C.c_int32), ("n_frames", C.c_int32), ("n_subch", C.c_int32),
+                ("threshold", C.c_int16), ("freq_sync_method", C.c_int16), ("subch", C.POINTER(Subch))]
+
+
+class StreamState(C.Structure):
+    _fields_ = [("next_pos", C.c_int64), ("local_phase", C.c_int32), ("coarse", C.c_int32),
+                ("fine", C.c_int16), ("f2correction", C.c_int16), ("prev1", C.c_int16), ("prev2", C.c_int16),
+                ("synced", C.c_int32), ("cif_count", C.c_int64), ("last_start_index", C.c_int32),
+                ("resyncs", C.c_int32)]
+
+
+_lib: Optional[C.CDLL] = None
+
+
+def lib() -> C.CDLL:
+    """Load libdabgpu.so (raises if it is missing: no silent fallback)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise DabError(f"{LIB_PATH} not built (run __graft_entry__.build())")
+        l = C.CDLL(LIB_PATH)
+        vp, i32, i64, sz = C.c_void_p, C.c_int, C.c_int64, C.c_size_t
+        sig = {
+            "dabgpu_abi_version": ([], i32), "dabgpu_last_error": ([], C.c_char_p),
+            "dabgpu_device_count": ([], i32), "dabgpu_ctx_create": ([i32, C.POINTER(vp)], i32),
+            "dabgpu_ctx_destroy": ([vp], i32), "dabgpu_sync": ([vp], i32),
+            "dabgpu_alloc": ([vp, sz, C.POINTER(vp)], i32), "dabgpu_free": ([vp, vp], i32),
+            "dabgpu_memcpy_h2d": ([vp, vp, vp, sz], i32), "dabgpu_memcpy_d2h": ([vp, vp, vp, sz], i32),
+            "dabgpu_memset_d": ([vp, vp, i32, sz], i32),
+            "dabgpu_event_record": ([vp, i32], i32),
+            "dabgpu_event_elapsed": ([vp, i32, i32, C.POINTER(C.c_float)], i32),
+            "dabgpu_prs_sync": ([vp, vp, vp, i32, C.c_int16, vp, vp, vp], i32),
+            "dabgpu_block0": ([vp, vp, vp, i32, vp], i32),
+            "dabgpu_ofdm_demod": ([vp, vp, vp, i32, vp, vp, vp], i32),
+            "dabgpu_viterbi": ([vp, vp, i32, i32, vp], i32),
+            "dabgpu_fic_decode": ([vp, vp, i32, vp, vp], i32),
+            "dabgpu_fic_decode_frames": ([vp, vp, vp, i32, vp, vp], i32),
+            "dabgpu_msc_deconvolve": ([vp, vp, i64, vp, i32, vp, i64], i32),
+            "dabgpu_pipe_create": ([vp, vp, C.POINTER(vp)], i32), "dabgpu_pipe_destroy": ([vp], i32),
+            "dabgpu_pipe_acquire": ([vp, vp, i64, vp, vp], i32),
+            "dabgpu_pipe_run": ([vp, vp, i64, vp, vp, vp, vp, C.c_int32, vp], i32),
+            "dabgpu_pipe_state": ([vp, i32, vp], i32),
+            "dabgpu_pipe_softbits": ([vp, C.POINTER(vp), C.POINTER(C.c_int32)], i32),
+            "dabgpu_pipe_frame_slot": ([vp, i32, C.POINTER(C.c_int32)], i32),
+            "dabgpu_pipe_frames": ([vp, vp, vp], i32),
+        }
+        for name, (args, res) in sig.items():
+            f = getattr(l, name)
+            f.argtypes, f.restype = args, res
+        _lib = l
+    return _lib
+
+
+def _chk(rc: int, what: str) -> None:
+    if rc != 0:
+        raise DabError(f"{what} failed ({rc}): {lib().dabgpu_last_error().decode()}")
+
+
+def _p(a: np.ndarray) -> C.c_void_p:
+    return C.c_void_p(a.ctypes.data)
+
+
+class DevBuf:
+    """HBM buffer owned by a Context."""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = C.c_void_p()
+        _chk(lib().dabgpu_alloc(ctx.h, max(self.nbytes, 16), C.byref(p)), "dabgpu_alloc")
+        self.ptr = p
+
+    def upload(self, a: np.ndarray) -> "DevBuf":
+        a = np.ascontiguousarray(a)
+        assert a.nbytes <= self.nbytes
+        _chk(lib().dabgpu_memcpy_h2d(self.ctx.h, self.ptr, _p(a), a.nbytes), "h2d")
+        return self
+
+    def download(self, dtype, shape) -> np.ndarray:
+        out = np.empty(shape, dtype=dtype)
+        assert out.nbytes <= self.nbytes
+        _chk(lib().dabgpu_memcpy_d2h(self.ctx.h, _p(out), self.ptr, out.nbytes), "d2h")
+        return out
+
+    def zero(self) -> "DevBuf":
+        _chk(lib().dabgpu_memset_d(self.ctx.h, self.ptr, 0, self.nbytes), "memset")
+        return self
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().dabgpu_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+
+class Context:
+    """One HIP device + stream (dabgpu_ctx)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        _chk(lib().dabgpu_ctx_create(device, C.byref(h)), "dabgpu_ctx_create")
+        self.h = h
+
+    def buf(self, nbytes: int) -> DevBuf:
+        return DevBuf(self, nbytes)
+
+    def put(self, a: np.ndarray) -> DevBuf:
+        a = np.ascontiguousarray(a)
+        return DevBuf(self, a.nbytes).upload(a)
+
+    def sync(self) -> None:
+        _chk(lib().dabgpu_sync(self.h), "sync")
+
+    def close(self) -> None:
+        if self.h:
+            lib().dabgpu_ctx_destroy(self.h)
+            self.h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        self.close()
+
+    # ---- operators mirroring the reference interfaces -------------------------
+    def viterbi(self, soft: np.ndarray, nbits: int) -> np.ndarray:
+        """viterbi::deconvolve (viterbi.cpp:225-242) for each row of soft [n, 4*(nbits+6)]."""
+        soft = np.ascontiguousarray(soft, dtype=np.int16).reshape(-1, 4 * (nbits + 6))
+        n = soft.shape[0]
+        din, dout = self.put(soft), self.buf(n * nbits)
+        try:
+            _chk(lib().dabgpu_viterbi(self.h, din.ptr, n, nbits, dout.ptr), "dabgpu_viterbi")
+            return dout.download(np.uint8, (n, nbits))
+        finally:
+            din.free(); dout.free()
+
+    def fic_process(self, blocks: np.ndarray):
+        """ficHandler::process_ficInput (fic-handler.cpp:241-321) for [n, 2304] soft bits.
+        Returns (bits [n,768] after energy dispersal and the CRC check's inversion, crc_ok [n,3])."""
+        blocks = np.ascontiguousarray(blocks, dtype=np.int16).reshape(-1, 2304)
+        n = blocks.shape[0]
+        din, db, dc = self.put(blocks), self.buf(n * 768), self.buf(n * 3)
+        try:
+            _chk(lib().dabgpu_fic_decode(self.h, din.ptr, n, db.ptr, dc.ptr), "dabgpu_fic_decode")
+            return db.download(np.uint8, (n, 768)), dc.download(np.uint8, (n, 3))
+        finally:
+            din.free(); db.free(); dc.free()
+
+    def msc_deconvolve(self, frags: np.ndarray, subch: Sequence[Subch]) -> list:
+        """uep_/eep_deconvolve::deconvolve + energy dispersal (deconvolve.cpp:172,325;
+        dab-concurrent.cpp:183-190): one already de-interleaved fragment per row."""
+        frags = np.ascontiguousarray(frags, dtype=np.int16)
+        n, stride = frags.shape
+        arr = (Subch * n)(*subch)
+        maxbits = max(24 * s.bitRate for s in subch)
+        din, dout = self.put(frags), self.buf(n * maxbits)
+        try:
+            _chk(lib().dabgpu_msc_deconvolve(self.h, din.ptr, stride, C.cast(arr, C.c_void_p), n, dout.ptr, maxbits),
+                 "dabgpu_msc_deconvolve")
+            out = dout.download(np.uint8, (n, maxbits))
+            return [out[i, :24 * subch[i].bitRate] for i in range(n)]
+        finally:
+            din.free(); dout.free()
+
+    def prs_sync(self, iq: DevBuf, frames: Sequence[Frame], level: int = 3):
+        """phaseReference::findIndex (phasereference.cpp:60-88) per frame window."""
+        n = len(frames)
+        fa = (Frame * n)(*frames)
+        dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
+        dsi, dmx, dsm = self.buf(4 * n), self.buf(4 * n), self.buf(4 * n)
+        try:
+            _chk(lib().dabgpu_prs_sync(self.h, iq.ptr, dfr.ptr, n, level, dsi.ptr, dmx.ptr, dsm.ptr), "prs_sync")
+            return (dsi.download(np.int32, n), dmx.download(np.float32, n), dsm.download(np.float32, n))
+        finally:
+            for b in (dfr, dsi, dmx, dsm):
+                b.free()
+
+    def block0(self, iq: DevBuf, frames: Sequence[Frame]) -> np.ndarray:
+        """ofdmDecoder::processBlock_0 coarse offset (ofdm-decoder.cpp:85-127)."""
+        n = len(frames)
+        fa = (Frame * n)(*frames)
+        dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
+        dc = self.buf(2 * n)
+        try:
+            _chk(lib().dabgpu_block0(self.h, iq.ptr, dfr.ptr, n, dc.ptr), "block0")
+            return dc.download(np.int16, n)
+        finally:
+            dfr.free(); dc.free()
+
+    def demod(self, iq: DevBuf, frames: Sequence[Frame], with_float: bool = False):
+        """ofdmDecoder::processToken for symbols 1..75 (ofdm-decoder.cpp:167-190).
+        Frame i must have out_slot == i.  Returns (ibits [n,75,3072], softf or None, freqcorr [n] complex)."""
+        n = len(frames)
+        fa = (Frame * n)(*frames)
+        dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
+        ds = self.buf(2 * n * NSYM * SYMBITS)
+        df = self.buf(4 * n * NSYM * SYMBITS) if with_float else None
+        dfc = self.buf(8 * n)
+        try:
+            _chk(lib().dabgpu_ofdm_demod(self.h, iq.ptr, dfr.ptr, n, ds.ptr, df.ptr if df else None, dfc.ptr),
+                 "ofdm_demod")
+            soft = ds.download(np.int16, (n, NSYM, SYMBITS))
+            softf = df.download(np.float32, (n, NSYM, SYMBITS)) if df else None
+            fc = dfc.download(np.float32, (n, 2))
+            return soft, softf, fc[:, 0] + 1j * fc[:, 1]
+        finally:
+            for b in (dfr, ds, df, dfc):
+                if b is not None:
+                    b.free()
+
+
+class Pipeline:
+    """ofdmProcessor::run + ficHandler + mscHandler for n_streams ensembles
+    (ofdm-processor.cpp:247-474, fic-handler.cpp:192-321, msc-handler.cpp:125-193,
+    dab-concurrent.cpp:144-193), n_frames frames per run() call."""
+
+    def __init__(self, ctx: Context, n_streams: int, n_frames: int, subch: Sequence[Subch],
+                 threshold: int = 3, freq_sync_method: int = 1):
+        self.ctx, self.S, self.F, self.subch = ctx, n_streams, n_frames, list(subch)
+        self._arr = (Subch * max(1, len(self.subch)))(*self.subch)
+        cfg = PipeCfg(n_streams, n_frames, len(self.subch), threshold, freq_sync_method,
+                      C.cast(self._arr, C.POINTER(Subch)))
+        h = C.c_void_p()
+        _chk(lib().dabgpu_pipe_create(ctx.h, C.byref(cfg), C.byref(h)), "dabgpu_pipe_create")
+        self.h = h
+        self.msc_stride = max([24 * s.bitRate for s in self.subch] + [768])
+        self.msc_stride = (self.msc_stride + 15) // 16 * 16
+        self.fic_d = ctx.buf(n_streams * n_frames * 4 * 768)
+        self.crc_d = ctx.buf(n_streams * n_frames * 12)
+        self.msc_d = ctx.buf(max(1, n_streams * 4 * n_frames * len(self.subch) * self.msc_stride))
+
+    def acquire(self, iq: DevBuf, stride: int, start: Sequence[int], n_avail: Sequence[int]) -> None:
+        st = np.asarray(start, dtype=np.int64)
+        na = np.asarray(n_avail, dtype=np.int64)
+        _chk(lib().dabgpu_pipe_acquire(self.h, iq.ptr, stride, _p(st), _p(na)), "dabgpu_pipe_acquire")
+
+    def run(self, iq: DevBuf, stride: int, n_avail: Sequence[int], download: bool = True):
+        na = np.asarray(n_avail, dtype=np.int64)
+        valid = np.zeros((self.S, 4 * self.F), dtype=np.uint8)
+        _chk(lib().dabgpu_pipe_run(self.h, iq.ptr, stride, _p(na), self.fic_d.ptr, self.crc_d.ptr,
+                                   self.msc_d.ptr if self.subch else None, self.msc_stride, _p(valid)),
+             "dabgpu_pipe_run")
+        if not download:
+            return valid
+        fic = self.fic_d.download(np.uint8, (self.S, self.F, 4, 768))
+        crc = self.crc_d.download(np.uint8, (self.S, self.F, 12))
+        msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), self.msc_stride)) \
+            if self.subch else None
+        return fic, crc, msc, valid
+
+    def state(self, s: int) -> StreamState:
+        o = StreamState()
+        _chk(lib().dabgpu_pipe_state(self.h, s, C.byref(o)), "dabgpu_pipe_state")
+        return o
+
+    def frames(self):
+        n = self.S * self.F
+        fr = (Frame * n)()
+        si = np.zeros(n, dtype=np.int32)
+        _chk(lib().dabgpu_pipe_frames(self.h, C.cast(fr, C.c_void_p), _p(si)), "dabgpu_pipe_frames")
+        return list(fr), si.reshape(self.S, self.F)
+
+    def softbits(self) -> np.ndarray:
+        p, r = C.c_void_p(), C.c_int32()
+        _chk(lib().dabgpu_pipe_softbits(self.h, C.byref(p), C.byref(r)), "softbits")
+        n = self.S * r.value * NSYM * SYMBITS
+        out = np.empty(n, dtype=np.int16)
+        _chk(lib().dabgpu_memcpy_d2h(self.ctx.h, _p(out), p, out.nbytes), "d2h")
+        return out.reshape(self.S, r.value, NSYM, SYMBITS)
+
+    def close(self) -> None:
+        if self.h:
+            for b in (self.fic_d, self.crc_d, self.msc_d):
+                b.free()
+            lib().dabgpu_pipe_destroy(self.h)
+            self.h = None

@@ -1,0 +1,100 @@
+"""TEST INFRASTRUCTURE: ctypes access to the CPU oracle (oracle/liboracle.so, our
+C restatement) and, when present, the reference's own compiled sources
+(oracle/_ref/libdabref.so).  Used only by tests/, smoke() and bench's CPU baseline."""
+import ctypes as C
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = os.path.join(ROOT, "oracle", "liboracle.so")
+REF = os.path.join(ROOT, "oracle", "_ref", "libdabref.so")
+
+
+class FrameInfo(C.Structure):
+    _fields_ = [("window_start", C.c_int64), ("start_index", C.c_int32), ("coarse", C.c_int32),
+                ("fine", C.c_int16), ("correction", C.c_int16), ("lp_window", C.c_int32)]
+
+
+def P(a):
+    return C.c_void_p(a.ctypes.data)
+
+
+_o = None
+_r = None
+
+
+def oracle():
+    global _o
+    if _o is None:
+        _o = C.CDLL(ORACLE)
+        _o.orc_get_phi.restype = C.c_float
+        _o.orc_find_index.restype = C.c_int32
+        _o.orc_process_block0.restype = C.c_int16
+        _o.orc_rs_dec.restype = C.c_int16
+        _o.orc_ofdm_run.argtypes = [C.c_void_p, C.c_int64, C.c_int16, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+    return _o
+
+
+def ref():
+    """reference sources compiled by oracle/Makefile (None when not built)."""
+    global _r
+    if _r is None and os.path.exists(REF):
+        _r = C.CDLL(REF)
+        _r.ref_get_phi.restype = C.c_float
+    return _r
+
+
+def viterbi(soft, nbits):
+    out = np.zeros(nbits, np.uint8)
+    oracle().orc_viterbi(P(np.ascontiguousarray(soft, np.int16)), nbits, P(out))
+    return out
+
+
+def fic_process(block):
+    bits = np.zeros(768, np.uint8)
+    ok = np.zeros(3, np.uint8)
+    oracle().orc_fic_process(P(np.ascontiguousarray(block, np.int16)), P(bits), P(ok))
+    return bits, ok
+
+
+def prbs(n):
+    out = np.zeros(n, np.uint8)
+    oracle().orc_prbs(n, P(out))
+    return out
+
+
+def msc_deconvolve(uep, bitrate, plevel, frag):
+    nb = 24 * bitrate
+    vb = np.zeros(4 * nb + 24, np.int16)
+    used = oracle().orc_msc_depuncture(uep, bitrate, plevel, P(np.ascontiguousarray(frag, np.int16)), P(vb))
+    assert used >= 0
+    out = viterbi(vb, nb)
+    return out ^ prbs(nb)
+
+
+def ofdm_run(iq, max_frames, threshold=3, method=1):
+    info = (FrameInfo * max_frames)()
+    soft = np.zeros((max_frames, 75, 3072), np.int16)
+    n = oracle().orc_ofdm_run(P(iq), C.c_int64(len(iq) // 2), threshold, method, max_frames, info, P(soft))
+    return n, list(info)[:n], soft[:n]
+
+
+def process_token(sym_ts, phase_ref):
+    """returns ibits, softf; updates phase_ref (cf32 float array [4096]) in place"""
+    ib = np.zeros(3072, np.int16)
+    sf = np.zeros(3072, np.float32)
+    oracle().orc_process_token(P(np.ascontiguousarray(sym_ts, np.float32)), P(phase_ref), P(ib), P(sf))
+    return ib, sf
+
+
+def process_block0(blk, flag=1, method=1):
+    pr = np.zeros(4096, np.float32)
+    c = oracle().orc_process_block0(P(np.ascontiguousarray(blk, np.float32)), P(pr), flag, method)
+    return c, pr
+
+
+def find_index(win, level=3):
+    mx, sm = C.c_float(), C.c_float()
+    r = oracle().orc_find_index(P(np.ascontiguousarray(win, np.float32)), level, C.byref(mx), C.byref(sm))
+    return r, mx.value, sm.value

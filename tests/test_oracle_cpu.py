@@ -1,0 +1,140 @@
+"""CPU tests: the oracle against the golden vectors produced by the reference's
+own sources, the oracle against the synthetic transmitter end to end, and
+the C ABI library's exported surface.  No GPU needed."""
+import ctypes as C
+import os
+import re
+
+import numpy as np
+import pytest
+
+import oracle_py as orc
+
+ROOT = orc.ROOT
+GOLD = os.path.join(ROOT, "tests", "golden")
+P = orc.P
+
+
+def _g(name):
+    return np.load(os.path.join(GOLD, name))
+
+
+def test_tables_match_reference_fixtures():
+    g = _g("tables.npz")
+    perm = np.zeros(1536, np.int16)
+    orc.oracle().orc_mapper(P(perm))
+    assert np.array_equal(perm, g["mapper"])
+    phi = np.array([orc.oracle().orc_get_phi(int(k)) for k in g["phi_k"]], np.float32)
+    assert np.array_equal(phi, g["phi"])
+    for i in range(24):
+        row = np.zeros(32, np.int8)
+        orc.oracle().orc_pcode(i + 1, P(row))
+        assert np.array_equal(row, g["pcodes"][i])
+
+
+def test_viterbi_matches_reference_fixtures():
+    g = _g("viterbi_kat.npz")
+    for nb in (768, 3072):
+        for soft, want in zip(g[f"in_{nb}"], g[f"out_{nb}"]):
+            assert np.array_equal(orc.viterbi(soft, nb), want)
+
+
+def test_msc_deconvolve_matches_reference_fixtures():
+    g = _g("msc_kat.npz")
+    for (uf, br, pl), frag, want in zip(g["cases"], g["frags"], g["out"]):
+        nb = 24 * int(br)
+        got = orc.msc_deconvolve(1 if uf == 0 else 0, int(br), int(pl), frag) ^ orc.prbs(nb)
+        assert np.array_equal(got, want[:nb]), (uf, br, pl)
+
+
+def test_rs_matches_reference_fixtures():
+    g = _g("rs_kat.npz")
+    for cw, dec, ret in zip(g["cw"], g["dec"], g["ret"]):
+        out = np.zeros(110, np.uint8)
+        r = C.c_int16(orc.oracle().orc_rs_dec(P(np.ascontiguousarray(cw)), P(out))).value
+        assert r == ret
+        if r >= 0:
+            assert np.array_equal(out, dec)
+
+
+def test_crc_and_firecode_match_reference_fixtures():
+    g = _g("crc_kat.npz")
+    for fib, ok, mut in zip(g["fibs"], g["crc"], g["mutated"]):
+        b = fib.copy()
+        assert orc.oracle().orc_check_crc_bits(P(b), 256) == ok
+        assert np.array_equal(b, mut)
+    for x, ok in zip(g["fire"], g["fire_ok"]):
+        assert orc.oracle().orc_firecode_check(P(np.ascontiguousarray(x))) == ok
+
+
+def test_oracle_decodes_synthetic_ensemble():
+    from dabamd.synth import Ensemble
+    subch = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 0)]
+    e = Ensemble(5, subch=subch)
+    g = e.generate(7)
+    n, info, soft = orc.ofdm_run(g["iq"], 5)
+    assert n == 5
+    assert all(fi.start_index == 504 for fi in info[1:])
+    assert np.array_equal((soft > 0).astype(np.uint8), g["coded"][:n])
+    for f in range(n):
+        fic = soft[f, 0:3].reshape(-1)
+        for b in range(4):
+            bits, ok = orc.fic_process(fic[2304 * b:2304 * (b + 1)])
+            assert ok.all()
+            want = g["fic"][f, b].copy()
+            for q in range(3):
+                want[256 * q + 240:256 * q + 256] ^= 1
+            assert np.array_equal(bits, want)
+    cifs = soft[:, 3:75].reshape(4 * n, -1)
+    for k, (sa, ln, br, pl, uep, _) in enumerate(subch):
+        frag = np.ascontiguousarray(cifs[:, sa * 64:(sa + ln) * 64])
+        out = np.zeros((4 * n, 24 * br), np.uint8)
+        assert orc.oracle().orc_msc_stream(uep, br, pl, ln * 64, 4 * n, P(frag), P(out)) == 0
+        for c in range(16, 4 * n):
+            assert np.array_equal(out[c], g["msc"][c, k, :24 * br])
+
+
+def test_oracle_dabplus_superframe():
+    """DAB+ superframes from the transmitter pass fire code, RS and AU CRCs in the oracle
+    (mp4processor.cpp:107-230)."""
+    from dabamd.synth import Ensemble
+    subch = [(0, 48, 64, 0o103, 0, 1)]
+    e = Ensemble(7, subch=subch)
+    g = e.generate(3)
+    bits = g["msc"][:, 0, :24 * 64]                  # CIF n carries encoder CIF n-15
+    # encoder CIF e = n - 15 and superframes start at e = -19 + 5m -> n = -4 + 5m
+    rs = 8
+    good = 0
+    for n0 in range(16, 4 * 7 - 4, 5):
+        if (n0 + 4) % 5:
+            continue
+        by = np.packbits(bits[n0:n0 + 5].reshape(-1))
+        assert orc.oracle().orc_firecode_check(P(by[:11]))
+        out = np.zeros(110 * rs, np.uint8)
+        nc = C.c_int16()
+        na = C.c_int()
+        au = np.zeros(8, np.int16)
+        crc = np.zeros(8, np.uint8)
+        ok = orc.oracle().orc_superframe(P(by), 0, 64, P(out), C.byref(nc), C.byref(na), P(au), P(crc))
+        assert ok == 1 and nc.value == 0 and na.value == 4 and crc[:4].all()
+        good += 1
+    assert good >= 2
+
+
+def test_abi_library_exports_every_declared_symbol():
+    hdr = open(os.path.join(ROOT, "include", "dabgpu.h")).read()
+    names = set(re.findall(r"\b(dabgpu_[a-z0-9_]+)\s*\(", hdr))
+    assert len(names) >= 25
+    import dabamd
+    lib = dabamd.lib()
+    for n in sorted(names):
+        assert hasattr(lib, n), n
+    assert lib.dabgpu_abi_version() == 1
+
+
+def test_abi_fails_loudly_without_device():
+    import dabamd
+    if dabamd.lib().dabgpu_device_count() > 0:
+        pytest.skip("device present")
+    with pytest.raises(dabamd.DabError):
+        dabamd.Context(0)
