@@ -194,6 +194,17 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, co
                     uint8_t *fic_bits_d, uint8_t *fic_crc_d, uint8_t *msc_bits_d, int32_t msc_stride,
                     uint8_t *msc_valid_h);
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
+/* per-stage kernel time of the last dabgpu_pipe_run (HIP events on the context
+ * stream; enabling it adds one stream synchronisation at the end of each run) */
+#define DABGPU_STAGE_PRS      0   /* k_prs_sync   (findIndex)          */
+#define DABGPU_STAGE_BLOCK0   1   /* k_block0     (processBlock_0 AFC) */
+#define DABGPU_STAGE_DEMOD    2   /* k_demod      (processToken x 75)  */
+#define DABGPU_STAGE_FIC      3   /* FIC Viterbi + CRC                 */
+#define DABGPU_STAGE_MSC_ACS  4   /* MSC Viterbi add-compare-select    */
+#define DABGPU_STAGE_MSC_TB   5   /* MSC chainback + energy dispersal  */
+#define DABGPU_NSTAGE         6
+int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on);
+int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms /*[DABGPU_NSTAGE]*/, int32_t *launches /*[DABGPU_NSTAGE] or NULL*/);
 /* device soft-bit ring of the last run ([n_streams][ring][75][3072]) and the slot of
  * (stream, frame) in it, for tests */
 int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft_d, int32_t *ring_frames);

@@ -94,6 +94,8 @@ hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int 
 hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
                           AcqResult *res);
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
+hipError_t launch_acs(hipStream_t st, const VitJob &job);
+hipError_t launch_traceback(hipStream_t st, const VitJob &job);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
 
 }  // namespace dab

@@ -192,7 +192,9 @@ int make_profile(const dabgpu_subch &s, Profile &p) {
     p.in_base[ns] = in;
     p.tail_mask = kPiXMask;
     p.frag = in + 12;
-    if (blk * 128 != 4 * p.nbits) return -2;  // profile inconsistent with bitRate
+    // an unknown UEP (bitRate, level) falls back to row 1 (deconvolve.cpp:150-153): its
+    // blocks then cover fewer than 4*nbits mother bits and the rest stays zero
+    if (blk * 128 > 4 * p.nbits) return -2;
     return 0;
 }
 
@@ -540,7 +542,30 @@ struct dabgpu_pipe {
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
     std::vector<int32_t> last_si;
+    // optional per-stage kernel timing (HIP events on the context stream)
+    bool profiling = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<int, int>> ev_rec;   // (stage, index of start event; end = +1)
+    float stage_ms[DABGPU_NSTAGE] = {};
+    int32_t stage_n[DABGPU_NSTAGE] = {};
 };
+
+static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
+    if (!p->profiling) return hipSuccess;
+    if (start) {
+        size_t need = 2 * (p->ev_rec.size() + 1);
+        while (p->ev_pool.size() < need) {
+            hipEvent_t e;
+            hipError_t r = hipEventCreate(&e);
+            if (r != hipSuccess) return r;
+            p->ev_pool.push_back(e);
+        }
+        int idx = (int)(2 * p->ev_rec.size());
+        p->ev_rec.push_back({stage, idx});
+        return hipEventRecord(p->ev_pool[idx], p->c->stream);
+    }
+    return hipEventRecord(p->ev_pool[p->ev_rec.back().second + 1], p->c->stream);
+}
 
 namespace {
 inline int32_t modM(int64_t x) {
@@ -618,6 +643,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
 int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     if (!p) return 0;
     (void)hipStreamSynchronize(p->c->stream);
+    for (auto e : p->ev_pool) (void)hipEventDestroy(e);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d})
         if (x) (void)hipFree(x);
@@ -720,7 +746,9 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     progress = false;
     if (n == 0) return 0;
     HIPCHK(hipMemcpyAsync(p->frames_d, fr.data(), sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
+    HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
     HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
+    HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
     std::vector<int32_t> si(n);
     HIPCHK(hipMemcpyAsync(si.data(), p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -755,7 +783,9 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     for (auto &d : fr2) if (d.flags & 1) any_f2 = true;
     if (n2 && any_f2) {
         HIPCHK(hipMemcpyAsync(p->frames_d, fr2.data(), sizeof(dabgpu_frame) * n2, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, true));
         HIPCHK(launch_block0(c->stream, iq, p->frames_d, n2, c->T, p->corr_d, general));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, false));
         HIPCHK(hipMemcpyAsync(corr.data(), p->corr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
     }
@@ -797,7 +827,9 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     std::vector<float2> fc(n3);
     if (n3) {
         HIPCHK(hipMemcpyAsync(p->frames_d, fr3.data(), sizeof(dabgpu_frame) * n3, hipMemcpyHostToDevice, c->stream));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
         HIPCHK(hipMemcpyAsync(fc.data(), p->fc_d, sizeof(float2) * n3, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipStreamSynchronize(c->stream));
@@ -868,6 +900,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     for (int s = 0; s < S; s++) if (!p->st[s].synced) return fail(DABGPU_E_STATE, "stream %d not synchronised", s);
     p->last_frames.assign((size_t)S * F, dabgpu_frame());
     p->last_si.assign((size_t)S * F, 0);
+    p->ev_rec.clear();
     std::vector<int> done(S, 0);
     std::vector<StreamSt> cur = p->st;
     bool lost = false;
@@ -904,8 +937,10 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             J.prbs_words = c->prbs;
             J.dec = p->dec_d;
             J.tiles_max = (768 + 6 + VCH - 1) / VCH;
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
             HIPCHK(launch_viterbi(c->stream, J));
             if (fic_crc) HIPCHK(launch_fic_post(c->stream, fic_bits, fic_crc, 12 * S * F));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         }
     }
     // MSC: all subchannels of all CIFs of this run
@@ -929,7 +964,12 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         J.prbs_words = c->prbs;
         J.dec = p->dec_d;
         J.tiles_max = (p->max_nbits + 6 + VCH - 1) / VCH;
-        HIPCHK(launch_viterbi(c->stream, J));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
+        HIPCHK(launch_acs(c->stream, J));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
+        HIPCHK(launch_traceback(c->stream, J));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
     }
     if (msc_valid)
         for (int s = 0; s < S; s++)
@@ -938,7 +978,31 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         cur[s].cif_count = p->st[s].cif_count + 4 * (int64_t)done[s];
     }
     p->st = cur;
+    if (p->profiling) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        for (int k = 0; k < DABGPU_NSTAGE; k++) { p->stage_ms[k] = 0.0f; p->stage_n[k] = 0; }
+        for (auto &r : p->ev_rec) {
+            float ms = 0.0f;
+            HIPCHK(hipEventElapsedTime(&ms, p->ev_pool[r.second], p->ev_pool[r.second + 1]));
+            p->stage_ms[r.first] += ms;
+            p->stage_n[r.first] += 1;
+        }
+    }
     if (lost || !all) return fail(DABGPU_E_STATE, "a stream lost sync or ran out of samples (see dabgpu_pipe_state)");
+    return 0;
+}
+
+int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on) {
+    if (!p) return fail(DABGPU_E_ARG, "null pipe");
+    p->profiling = on != 0;
+    return 0;
+}
+int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
+    if (!p || !ms) return fail(DABGPU_E_ARG, "bad args");
+    for (int k = 0; k < DABGPU_NSTAGE; k++) {
+        ms[k] = p->stage_ms[k];
+        if (launches) launches[k] = p->stage_n[k];
+    }
     return 0;
 }
 

@@ -95,6 +95,11 @@ __device__ __forceinline__ void fetch4(const VitJob &J, const CwInfo &c, const P
         base = P.in_base[s] + bis * 4 * n1 + (o >> 5) * n1;
     } else {
         b = p - 128 * P.blk_end[P.nseg - 1];
+        if (b >= 24) {                               // beyond PI_X: the memset zeros of the
+#pragma unroll                                       // viterbiBlock (deconvolve.cpp:182)
+            for (int e = 0; e < 4; e++) x[e] = 0;
+            return;
+        }
         m = P.tail_mask;
         base = P.in_base[P.nseg];
     }
@@ -234,6 +239,17 @@ hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     hipLaunchKernelGGL(k_acs, dim3(job.n_cw), dim3(64), 0, st, job);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_traceback, dim3((job.n_cw + 63) / 64), dim3(64), 0, st, job);
+    return hipGetLastError();
+}
+
+hipError_t launch_acs(hipStream_t st, const VitJob &job) {
+    if (job.n_cw <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_acs, dim3(job.n_cw), dim3(64), 0, st, job);
+    return hipGetLastError();
+}
+hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
+    if (job.n_cw <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_traceback, dim3((job.n_cw + 63) / 64), dim3(64), 0, st, job);
     return hipGetLastError();
 }

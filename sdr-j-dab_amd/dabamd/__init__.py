@@ -86,6 +86,8 @@ def lib() -> C.CDLL:
             "dabgpu_pipe_softbits": ([vp, C.POINTER(vp), C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frame_slot": ([vp, i32, C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frames": ([vp, vp, vp], i32),
+            "dabgpu_pipe_set_profiling": ([vp, i32], i32),
+            "dabgpu_pipe_timing": ([vp, vp, vp], i32),
         }
         for name, (args, res) in sig.items():
             f = getattr(l, name)
@@ -288,6 +290,18 @@ class Pipeline:
         msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), self.msc_stride)) \
             if self.subch else None
         return fic, crc, msc, valid
+
+    STAGES = ("prs_sync", "block0", "demod", "fic", "msc_acs", "msc_traceback")
+
+    def set_profiling(self, on: bool = True) -> None:
+        _chk(lib().dabgpu_pipe_set_profiling(self.h, 1 if on else 0), "set_profiling")
+
+    def timing(self) -> dict:
+        """per-stage kernel milliseconds and launch counts of the last run()"""
+        ms = np.zeros(len(self.STAGES), np.float32)
+        n = np.zeros(len(self.STAGES), np.int32)
+        _chk(lib().dabgpu_pipe_timing(self.h, _p(ms), _p(n)), "timing")
+        return {k: (float(ms[i]), int(n[i])) for i, k in enumerate(self.STAGES)}
 
     def state(self, s: int) -> StreamState:
         o = StreamState()
