@@ -131,7 +131,7 @@ def main():
     from dabamd.synth import Ensemble
 
     E, F = args.ensembles, args.frames
-    total_frames = F * (args.warmup + args.steps) + 1
+    total_frames = F * (args.warmup + args.steps + 1) + 1   # +1 step: the profiled pass
     ens = Ensemble(total_frames, subch=C3_SUBCH, snr_db=30.0)
     t0 = time.time()
     iq = ens.generate_many(E, seed0=1000 + rank * E, threads=min(16, os.cpu_count() or 1))

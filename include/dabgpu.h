@@ -39,6 +39,7 @@ extern "C" {
 #define DABGPU_E_NOMEM    -4
 #define DABGPU_E_UNSUP    -5   /* configuration the reference does not define */
 #define DABGPU_E_STATE    -6   /* call out of sequence */
+#define DABGPU_E_BOUNDS   -7   /* a kernel refused a descriptor that points outside its stream */
 
 /* Mode-I geometry (gui.cpp:1361-1371) */
 #define DABGPU_TU     2048
@@ -72,6 +73,7 @@ typedef struct {
  * sample is multiplied by oscillatorTable[localPhase]. */
 typedef struct {
     int64_t iq_base;    /* element offset (cf32 units) of the stream in the IQ buffer */
+    int64_t n_samples;  /* samples of this stream readable from iq_base (bounds check) */
     int64_t window;     /* first sample of the T_u sync window (SyncOnPhase) */
     int64_t block0;     /* first sample of block 0 = window + startIndex */
     int32_t lp_window;  /* localPhase before the window's first sample */
@@ -96,6 +98,8 @@ int         dabgpu_memcpy_d2h(dabgpu_ctx *ctx, void *dst_h, const void *src_d, s
 int         dabgpu_memset_d(dabgpu_ctx *ctx, void *dst_d, int value, size_t bytes);
 /* HIP events on the context stream, for timing (ms between two marks) */
 int         dabgpu_event_record(dabgpu_ctx *ctx, int slot);
+/* device-side bounds violations flagged by kernels since the last call (syncs; clears) */
+int         dabgpu_kernel_errors(dabgpu_ctx *ctx);
 int         dabgpu_event_elapsed(dabgpu_ctx *ctx, int slot_a, int slot_b, float *ms);
 
 /* ---- OFDM front end (L3) ---------------------------------------------- */

@@ -20,7 +20,10 @@ struct OfdmTables {
     const float2 *ref_l;    // PRS refTable in FFT output lane layout [i][lane]
     const uint32_t *cmap_l; // carrier of FFT bin, lane layout [i/2][lane], two int16 per word (-1 unused)
     const float *refarg;    // refArg[18] (ofdm-decoder.cpp:71-74)
+    int32_t *err;           // device error word: kernels OR in DABGPU_KERR_* bits
 };
+constexpr int KERR_FRAME = 1;      // frame descriptor outside its stream / bad NCO phase
+constexpr int KERR_VITERBI = 2;    // Viterbi source outside its buffer
 
 struct AcqJob {
     int64_t iq_base;
@@ -63,6 +66,8 @@ struct VitJob {
     int32_t kind;
     int32_t n_cw;
     const int16_t *src;
+    int64_t src_len;        // elements readable from src (bounds check)
+    int32_t *err;           // device error word
     int64_t src_stride;     // SRC_MOTHER / SRC_FRAG: elements per codeword
     const Profile *prof;    // per-profile table
     const int32_t *cw_prof; // SRC_FRAG: profile per codeword; else null (profile 0 / by subch)

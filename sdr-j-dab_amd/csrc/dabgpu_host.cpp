@@ -225,6 +225,7 @@ struct dabgpu_ctx {
     float2 *osc = nullptr, *tw = nullptr, *ref_l = nullptr;
     uint32_t *cmap_l = nullptr, *prbs = nullptr;
     float *refarg = nullptr;
+    int32_t *err = nullptr;      // device error word (KERR_* bits)
     OfdmTables T{};
     // growable scratch
     void *scratch[8] = {};
@@ -244,6 +245,17 @@ static int scratch(dabgpu_ctx *c, int slot, size_t bytes, void **p) {
     return 0;
 }
 enum { SC_DEC = 0, SC_PROF = 1, SC_I32 = 2, SC_FRAMES = 3, SC_FC = 4, SC_MISC = 5 };
+
+// read (and clear) the device error word; call after a stream synchronisation
+static int kernel_errors(dabgpu_ctx *c) {
+    int32_t e = 0;
+    HIPCHK(hipMemcpyAsync(&e, c->err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    if (!e) return 0;
+    HIPCHK(hipMemsetAsync(c->err, 0, sizeof(int32_t), c->stream));
+    return fail(DABGPU_E_BOUNDS, "kernel refused out-of-bounds work:%s%s", (e & KERR_FRAME) ? " frame descriptor" : "",
+                (e & KERR_VITERBI) ? " viterbi source" : "");
+}
 
 template <class T>
 static int upload(dabgpu_ctx *c, T **dst, const std::vector<T> &v) {
@@ -291,6 +303,11 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     c->T.ref_l = c->ref_l;
     c->T.cmap_l = c->cmap_l;
     c->T.refarg = c->refarg;
+    if (hipMalloc((void **)&c->err, sizeof(int32_t)) != hipSuccess || hipMemset(c->err, 0, sizeof(int32_t)) != hipSuccess) {
+        dabgpu_ctx_destroy(c);
+        return fail(DABGPU_E_HIP, "error word alloc");
+    }
+    c->T.err = c->err;
     *out = c;
     return 0;
 }
@@ -300,7 +317,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->cmap_l, (void *)c->prbs,
-                    (void *)c->refarg})
+                    (void *)c->refarg, (void *)c->err})
         if (p) (void)hipFree(p);
     for (auto p : c->scratch) if (p) (void)hipFree(p);
     for (auto e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -342,6 +359,11 @@ int dabgpu_memset_d(dabgpu_ctx *c, void *dst, int value, size_t bytes) {
     HIPCHK(hipMemsetAsync(dst, value, bytes, c->stream));
     return 0;
 }
+int dabgpu_kernel_errors(dabgpu_ctx *c) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    return kernel_errors(c);
+}
+
 int dabgpu_event_record(dabgpu_ctx *c, int slot) {
     if (!c || slot < 0 || slot >= 16) return fail(DABGPU_E_ARG, "bad event slot");
     HIPCHK(hipEventRecord(c->ev[slot], c->stream));
@@ -391,6 +413,7 @@ static int run_viterbi(dabgpu_ctx *c, VitJob &J, int max_nbits) {
     J.dec = (uint64_t *)dec;
     J.tiles_max = tiles;
     J.prbs_words = c->prbs;
+    J.err = c->err;
     HIPCHK(launch_viterbi(c->stream, J));
     return 0;
 }
@@ -410,6 +433,7 @@ int dabgpu_viterbi(dabgpu_ctx *c, const int16_t *in, int n_cw, int nbits, uint8_
     J.n_cw = n_cw;
     J.src = in;
     J.src_stride = 4 * (int64_t)(nbits + 6);
+    J.src_len = (int64_t)n_cw * J.src_stride;
     J.prof = (const Profile *)pd;
     J.out = out;
     J.out_stride = nbits;
@@ -440,6 +464,7 @@ int dabgpu_fic_decode(dabgpu_ctx *c, const int16_t *soft, int n, uint8_t *bits, 
     J.n_cw = n;
     J.src = soft;
     J.src_stride = 2304;
+    J.src_len = (int64_t)n * 2304;
     return fic_common(c, J, bits, ok);
 }
 
@@ -456,10 +481,17 @@ int dabgpu_fic_decode_frames(dabgpu_ctx *c, const int16_t *soft, const int32_t *
     J.n_cw = 4 * nf;
     J.src = soft;
     J.slots = (const int32_t *)sd;
+    {
+        int32_t mx = 0;
+        for (int i = 0; i < nf; i++) {
+            if (slots_h[i] < 0) return fail(DABGPU_E_ARG, "negative slot");
+            mx = std::max(mx, slots_h[i]);
+        }
+        J.src_len = (int64_t)(mx + 1) * FRAME_SOFT;
+    }
     rc = fic_common(c, J, bits, ok);
     if (rc) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));       // slots scratch may be reused by the next call
-    return 0;
+    return kernel_errors(c);                       // also: slots scratch may be reused by the next call
 }
 
 int dabgpu_msc_deconvolve(dabgpu_ctx *c, const int16_t *frag, int64_t frag_stride, const dabgpu_subch *sub,
@@ -494,14 +526,14 @@ int dabgpu_msc_deconvolve(dabgpu_ctx *c, const int16_t *frag, int64_t frag_strid
     J.n_cw = n_cw;
     J.src = frag;
     J.src_stride = frag_stride;
+    J.src_len = (int64_t)n_cw * frag_stride;
     J.prof = (const Profile *)pd;
     J.cw_prof = (const int32_t *)cd;
     J.out = bits;
     J.out_stride = out_stride;
     J.prbs = 1;
     if ((rc = run_viterbi(c, J, maxbits))) return rc;
-    HIPCHK(hipStreamSynchronize(c->stream));
-    return 0;
+    return kernel_errors(c);
 }
 
 }  // extern "C"
@@ -712,6 +744,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
             const int32_t si = x.last_si;
             const int32_t pa = x.coarse + x.fine;
             d.iq_base = stride * s;
+            d.n_samples = n_avail[s];
             d.window = x.window;
             d.block0 = x.window + si;
             d.lp_window = x.lp;
@@ -751,7 +784,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
     std::vector<int32_t> si(n);
     HIPCHK(hipMemcpyAsync(si.data(), p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
-    HIPCHK(hipStreamSynchronize(c->stream));
+    if (int rc = kernel_errors(c)) return rc;
     // pass 1: windows.  A frame is usable if every earlier frame of its stream
     // had the predicted startIndex; its own startIndex fixes block0.
     std::vector<char> ok(n, 0);
@@ -764,6 +797,10 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
             if (!valid) continue;
             if (si[i] < 0) {               // sync lost (ofdm-processor.cpp:354-357)
                 valid = false;
+                continue;
+            }
+            if (fr[i].window + si[i] + TU + (int64_t)NSYM * TS + TNULL > n_avail[fs[i]]) {
+                valid = false;             // the frame would run past the stream's samples
                 continue;
             }
             ok[i] = 1;
@@ -787,7 +824,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         HIPCHK(launch_block0(c->stream, iq, p->frames_d, n2, c->T, p->corr_d, general));
         HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, false));
         HIPCHK(hipMemcpyAsync(corr.data(), p->corr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        if (int rc = kernel_errors(c)) return rc;
     }
     // replay the coarse corrector with the measured corrections; phase_b of a
     // frame uses its own correction, later frames are cut if the corrector moved
@@ -832,7 +869,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
         HIPCHK(hipMemcpyAsync(fc.data(), p->fc_d, sizeof(float2) * n3, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipStreamSynchronize(c->stream));
+        if (int rc = kernel_errors(c)) return rc;
     }
     // commit: replay the full per-frame state update (ofdm-processor.cpp:395-468)
     {
@@ -929,6 +966,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             J.kind = SRC_FIC;
             J.n_cw = 4 * S * F;
             J.src = p->ring;
+            J.src_len = (int64_t)S * p->R * FRAME_SOFT;
+            J.err = c->err;
             J.slots = p->slots_d;
             J.prof = (const Profile *)pd;
             J.out = fic_bits;
@@ -952,6 +991,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         J.kind = SRC_MSC;
         J.n_cw = S * 4 * F * p->NSUB;
         J.src = p->ring;
+        J.src_len = (int64_t)S * p->R * FRAME_SOFT;
+        J.err = c->err;
         J.prof = p->prof_d;
         J.nsub = p->NSUB;
         J.ncif = 4 * F;

@@ -46,6 +46,14 @@ __device__ __forceinline__ void load_mixed(const float2 *__restrict__ s, int64_t
     }
 }
 
+// a frame descriptor must keep every read inside its stream (else: flag + skip)
+__device__ __forceinline__ bool frame_ok(const dabgpu_frame &fr, int64_t last_excl, int32_t *err) {
+    const bool ok = fr.window >= 0 && fr.block0 >= fr.window && last_excl <= fr.n_samples &&
+                    fr.lp_window >= 0 && fr.lp_window < INPUT_RATE && fr.lp_data >= 0 && fr.lp_data < INPUT_RATE;
+    if (!ok && threadIdx.x == 0) atomicOr(err, KERR_FRAME);
+    return ok;
+}
+
 // trunc((double)q * 127.0) computed exactly in fp32 (ofdm-decoder.cpp:188-189)
 __device__ __forceinline__ int trunc127(float q) {
     float hi = __fmul_rn(q, 127.0f);
@@ -64,6 +72,10 @@ __global__ __launch_bounds__(64) void k_prs_sync(const float2 *__restrict__ iq,
     const int lane = threadIdx.x, f = blockIdx.x;
     if (f >= n) return;
     const dabgpu_frame fr = frames[f];
+    if (!frame_ok(fr, fr.window + TU, T.err)) {
+        if (lane == 0) start_index[f] = -1;
+        return;
+    }
     const float2 *s = iq + fr.iq_base;
     Twiddles tw;
     load_twiddles(tw, T.tw, lane);
@@ -120,6 +132,10 @@ __global__ __launch_bounds__(64) void k_block0(const float2 *__restrict__ iq,
         if (lane == 0) correction[f] = 0;
         return;
     }
+    if (!frame_ok(fr, fr.block0 + TU, T.err)) {
+        if (lane == 0) correction[f] = 0;
+        return;
+    }
     const float2 *s = iq + fr.iq_base;
     Twiddles tw;
     load_twiddles(tw, T.tw, lane);
@@ -165,7 +181,7 @@ __global__ __launch_bounds__(64, DEMOD_WAVES) void k_demod(const float2 *__restr
     const int per = (NSYM + nchunks - 1) / nchunks;
     const int l0 = 1 + ch * per, l1 = min(NSYM + 1, l0 + per);
     float2 fc = make_float2(0.0f, 0.0f);
-    if (l0 <= NSYM) {
+    if (l0 <= NSYM && frame_ok(fr, fr.block0 + TU + (int64_t)NSYM * TS, T.err)) {
         const int64_t dorg = fr.block0 + TU;       // first sample of segment B
         Twiddles tw;
         load_twiddles(tw, T.tw, lane);

@@ -64,12 +64,21 @@ __device__ __forceinline__ CwInfo cw_info(const VitJob &J, int cw) {
 
 // soft value of punctured-input element idx of codeword c
 __device__ __forceinline__ int load_elem(const VitJob &J, const CwInfo &c, int idx) {
-    if (J.kind != SRC_MSC) return c.base[idx];
-    const int64_t g = c.cif - delay16(idx);
-    if (g < 0) return 0;                              // delay lines start at zero
-    const int64_t frame = g >> 2;
-    const int slot = (int)(frame % J.ring);
-    return J.src[c.stream_off + ((int64_t)slot * NSYM + 3 + 18 * (int)(g & 3)) * SYMBITS + c.sub_start + idx];
+    int64_t off;
+    if (J.kind != SRC_MSC) {
+        off = (c.base - J.src) + idx;
+    } else {
+        const int64_t g = c.cif - delay16(idx);
+        if (g < 0) return 0;                          // delay lines start at zero
+        const int64_t frame = g >> 2;
+        const int slot = (int)(frame % J.ring);
+        off = c.stream_off + ((int64_t)slot * NSYM + 3 + 18 * (int)(g & 3)) * SYMBITS + c.sub_start + idx;
+    }
+    if (off < 0 || off >= J.src_len) {               // never read outside the buffer
+        atomicOr(J.err, KERR_VITERBI);
+        return 0;
+    }
+    return J.src[off];
 }
 
 // the 4 mother-code soft values of trellis step t (positions 4t..4t+3)
@@ -78,7 +87,7 @@ __device__ __forceinline__ void fetch4(const VitJob &J, const CwInfo &c, const P
     const int p = 4 * t;
     if (P.nseg == 0) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) x[e] = c.base[p + e];
+        for (int e = 0; e < 4; e++) x[e] = load_elem(J, c, p + e);
         return;
     }
     const int blk = p >> 7;

