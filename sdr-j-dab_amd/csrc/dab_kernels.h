@@ -77,7 +77,7 @@ struct VitJob {
     int32_t nsub, ncif, ring;      // subchannels, CIFs in this batch, ring frames
     int64_t cif0;                   // global CIF index of the batch's first CIF (per stream, same for all)
     int32_t first_slot;             // ring slot of the batch's first frame
-    const int16_t *sub_start;       // startAddr*64 per subchannel
+    const int32_t *sub_start;       // startAddr*64 per subchannel (up to 55232: int32)
     // outputs
     uint64_t *dec;                  // decision tiles
     const int64_t *dec_off;         // per-codeword tile offset (u64 units); null: cw * tiles_max * VCH

@@ -563,7 +563,7 @@ struct dabgpu_pipe {
     std::vector<StreamSt> st;
     int16_t *ring = nullptr;         // [S][R][75][3072]
     Profile *prof_d = nullptr;       // [NSUB]
-    int16_t *substart_d = nullptr;   // [NSUB]
+    int32_t *substart_d = nullptr;   // [NSUB]
     dabgpu_frame *frames_d = nullptr;
     int32_t *si_d = nullptr;
     int16_t *corr_d = nullptr;
@@ -625,7 +625,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     p->sub.assign(cfg->subch, cfg->subch + cfg->n_subch);
     p->st.assign(p->S, StreamSt());
     std::vector<Profile> profs(std::max(1, p->NSUB));
-    std::vector<int16_t> ss(std::max(1, p->NSUB), 0);
+    std::vector<int32_t> ss(std::max(1, p->NSUB), 0);
     p->max_nbits = 768;
     for (int i = 0; i < p->NSUB; i++) {
         if (make_profile(p->sub[i], profs[i])) {
@@ -636,7 +636,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
             delete p;
             return fail(DABGPU_E_ARG, "subchannel %d does not fit its CUs", i);
         }
-        ss[i] = (int16_t)(p->sub[i].startAddr * 64);
+        ss[i] = p->sub[i].startAddr * 64;
         p->max_nbits = std::max(p->max_nbits, profs[i].nbits);
     }
     const size_t SF = (size_t)p->S * p->F;
@@ -647,7 +647,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     };
     A((void **)&p->ring, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT);
     A((void **)&p->prof_d, sizeof(Profile) * profs.size());
-    A((void **)&p->substart_d, sizeof(int16_t) * ss.size());
+    A((void **)&p->substart_d, sizeof(int32_t) * ss.size());
     A((void **)&p->frames_d, sizeof(dabgpu_frame) * SF);
     A((void **)&p->si_d, sizeof(int32_t) * SF);
     A((void **)&p->corr_d, sizeof(int16_t) * SF);
@@ -660,7 +660,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->dec_d, p->dec_sz);
     if (!rc) {
         if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(p->substart_d, ss.data(), sizeof(int16_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(p->substart_d, ss.data(), sizeof(int32_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemset(p->ring, 0, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
             rc = fail(DABGPU_E_HIP, "pipe init copy failed");
     }

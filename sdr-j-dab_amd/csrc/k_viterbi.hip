@@ -72,7 +72,12 @@ __device__ __forceinline__ int load_elem(const VitJob &J, const CwInfo &c, int i
         if (g < 0) return 0;                          // delay lines start at zero
         const int64_t frame = g >> 2;
         const int slot = (int)(frame % J.ring);
-        off = c.stream_off + ((int64_t)slot * NSYM + 3 + 18 * (int)(g & 3)) * SYMBITS + c.sub_start + idx;
+        const int64_t loc = ((int64_t)slot * NSYM + 3 + 18 * (int)(g & 3)) * SYMBITS + c.sub_start + idx;
+        if (loc < 0 || loc >= (int64_t)J.ring * FRAME_SOFT) {   // stay inside this stream's ring
+            atomicOr(J.err, KERR_VITERBI);
+            return 0;
+        }
+        off = c.stream_off + loc;
     }
     if (off < 0 || off >= J.src_len) {               // never read outside the buffer
         atomicOr(J.err, KERR_VITERBI);

@@ -216,7 +216,8 @@ def _pipeline_decode(ctx, ens_list, F, subch, cfo=0.0, snr=300.0, runs=2):
 
 
 def test_pipeline_end_to_end(ctx):
-    subch = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 0), (144, 96, 128, 3, 1, 0)]
+    # the last subchannel sits above CU 512 (startAddr*64 > 32767)
+    subch = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 0), (768, 96, 128, 3, 1, 0)]
     F = 4
     gens, outs, states = _pipeline_decode(ctx, [101, 102], F, subch, snr=300.0, runs=2)
     for s, g in enumerate(gens):
