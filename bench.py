@@ -127,6 +127,10 @@ def main():
     args = ap.parse_args()
 
     rank, local, world, dist = dist_setup(args.gpus)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # before this process touches the GPU: the workers are forked children
+        cpu = cpu_baseline(budget_s=args.cpu_seconds)
     import dabamd
     from dabamd.synth import Ensemble
 
@@ -202,8 +206,8 @@ def main():
         "fic_crc_pass_rate": crc_ok,
         "gen_seconds": gen_s,
     }
-    if not args.no_cpu_baseline:
-        v, cores, kind, syms = cpu_baseline(budget_s=args.cpu_seconds)
+    if cpu is not None:
+        v, cores, kind, syms = cpu
         out["cpu_baseline"] = {"value": v, "unit": "symbols/s", "cores": cores, "kind": kind,
                                "sample": f"{cores} workers x own synthetic C3 ensemble (6 frames, 9 UEP-3 128k "
                                          f"subch), ~{args.cpu_seconds:.0f}s each, {syms} symbols total; "

@@ -749,8 +749,10 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
             d.block0 = x.window + si;
             d.lp_window = x.lp;
             d.phase_a = pa;
+            // the reference reads the T_u window first (ofdm-processor.cpp:344-352); whether
+            // the rest of the frame is there is known once startIndex is (pass 1)
+            if (d.window + TU > n_avail[s]) break;
             int64_t end = d.block0 + TU + (int64_t)NSYM * TS + TNULL;
-            if (end > n_avail[s]) break;                       // not enough samples for this frame
             // f2 logic with the predicted correction 0 (ofdm-processor.cpp:395-406)
             d.flags = x.f2 ? 1 : 0;
             bool f2 = x.f2;
@@ -799,10 +801,12 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
                 valid = false;
                 continue;
             }
-            if (fr[i].window + si[i] + TU + (int64_t)NSYM * TS + TNULL > n_avail[fs[i]]) {
-                valid = false;             // the frame would run past the stream's samples
+            if (fr[i].window + si[i] + TU + (int64_t)NSYM * TS > n_avail[fs[i]]) {
+                valid = false;             // symbols 1..75 not all there yet: wait for samples
                 continue;
             }
+            // (the null symbol after the frame is skipped when the next frame is read,
+            // as the reference's getSamples(T_null) does, ofdm-processor.cpp:449-453)
             ok[i] = 1;
             fr[i].block0 = fr[i].window + si[i];
             fr[i].lp_data = lp_after(fr[i].lp_window, (int64_t)TU + si[i], fr[i].phase_a);
