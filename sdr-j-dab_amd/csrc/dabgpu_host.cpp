@@ -406,12 +406,12 @@ int dabgpu_ofdm_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, in
 
 // ---- Viterbi operators -------------------------------------------------------
 static int run_viterbi(dabgpu_ctx *c, VitJob &J, int max_nbits) {
-    const int tiles = (max_nbits + 6 + VCH - 1) / VCH;
+    const int64_t ds = dec_stride_for(max_nbits);
     void *dec = nullptr;
-    int rc = scratch(c, SC_DEC, sizeof(uint64_t) * (size_t)J.n_cw * tiles * VCH, &dec);
+    int rc = scratch(c, SC_DEC, sizeof(uint64_t) * (size_t)J.n_cw * ds, &dec);
     if (rc) return rc;
     J.dec = (uint64_t *)dec;
-    J.tiles_max = tiles;
+    J.dec_stride = ds;
     J.prbs_words = c->prbs;
     J.err = c->err;
     HIPCHK(launch_viterbi(c->stream, J));
@@ -654,9 +654,8 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->fc_d, sizeof(float2) * SF);
     A((void **)&p->fcpart_d, sizeof(float2) * SF * kChunks);
     A((void **)&p->slots_d, sizeof(int32_t) * SF);
-    const int tiles = (p->max_nbits + 6 + VCH - 1) / VCH;
     const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
-    p->dec_sz = sizeof(uint64_t) * ncw * tiles * VCH;
+    p->dec_sz = sizeof(uint64_t) * ncw * (size_t)dec_stride_for(p->max_nbits);
     A((void **)&p->dec_d, p->dec_sz);
     if (!rc) {
         if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -979,7 +978,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             J.prbs = 1;
             J.prbs_words = c->prbs;
             J.dec = p->dec_d;
-            J.tiles_max = (768 + 6 + VCH - 1) / VCH;
+            J.dec_stride = dec_stride_for(768);
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
             HIPCHK(launch_viterbi(c->stream, J));
             if (fic_crc) HIPCHK(launch_fic_post(c->stream, fic_bits, fic_crc, 12 * S * F));
@@ -1008,7 +1007,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         J.prbs = 1;
         J.prbs_words = c->prbs;
         J.dec = p->dec_d;
-        J.tiles_max = (p->max_nbits + 6 + VCH - 1) / VCH;
+        J.dec_stride = dec_stride_for(p->max_nbits);
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
         HIPCHK(launch_acs(c->stream, J));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));

@@ -29,70 +29,102 @@ __device__ __forceinline__ int delay16(int i) {         // dab-concurrent.cpp:42
     return 15 - rv;
 }
 
-struct CwInfo {
-    int prof;
+// XCD-aware block order (cdna_hip_programming.md T1): blocks b with equal b % 8
+// share an XCD's L2; give each such group a contiguous range of codewords so the
+// 16 CIFs that read the same ring rows (time de-interleave) decode on one L2.
+__device__ __forceinline__ int xcd_order(int b, int n) {
+    const int q = n >> 3, r = n & 7, x = b & 7;
+    return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+// Per-codeword source, resolved once per wave.
+struct Src {
+    const int16_t *base;   // first input element (SRC_MSC: the stream's ring)
+    int prof;              // profile index
+    int row;               // output / decision row of this codeword
     bool valid;
-    // source addressing
-    const int16_t *base;   // for SRC_MOTHER/FRAG/FIC
-    int64_t stream_off;    // SRC_MSC: element offset of the stream's ring
-    int64_t cif;           // SRC_MSC: global CIF index
-    int32_t sub_start;
 };
 
-__device__ __forceinline__ CwInfo cw_info(const VitJob &J, int cw) {
-    CwInfo c;
-    c.prof = 0; c.valid = true; c.base = nullptr; c.stream_off = 0; c.cif = 0; c.sub_start = 0;
-    switch (J.kind) {
-    case SRC_MOTHER: c.base = J.src + (int64_t)cw * J.src_stride; break;
-    case SRC_FRAG:   c.base = J.src + (int64_t)cw * J.src_stride; c.prof = J.cw_prof ? J.cw_prof[cw] : 0; break;
-    case SRC_FIC:    c.base = J.src + (int64_t)J.slots[cw >> 2] * FRAME_SOFT + (cw & 3) * 2304; break;
-    default: {
-        const int sub = cw % J.nsub;
-        const int rest = cw / J.nsub;
-        const int cl = rest % J.ncif;
-        const int stream = rest / J.ncif;
+// SRC_MSC logical order (stream, subchannel, CIF) -- consecutive CIFs of one
+// subchannel share 15 of their 16 source rows; output rows stay
+// ((stream * ncif) + cif) * nsub + sub.
+template <int KIND>
+__device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *rowoff, int lane) {
+    Src c;
+    c.prof = 0;
+    c.valid = true;
+    c.row = logical;
+    if constexpr (KIND == SRC_MOTHER) {
+        c.base = J.src + (int64_t)logical * J.src_stride;
+    } else if constexpr (KIND == SRC_FRAG) {
+        c.base = J.src + (int64_t)logical * J.src_stride;
+        c.prof = J.cw_prof ? J.cw_prof[logical] : 0;
+    } else if constexpr (KIND == SRC_FIC) {
+        c.base = J.src + (int64_t)J.slots[logical >> 2] * FRAME_SOFT + (logical & 3) * 2304;
+    } else {
+        const int cl = logical % J.ncif;
+        const int rest = logical / J.ncif;
+        const int sub = rest % J.nsub;
+        const int stream = rest / J.nsub;
+        c.row = (stream * J.ncif + cl) * J.nsub + sub;
         c.prof = sub;
-        c.cif = J.cif0 + cl;
-        c.valid = c.cif >= 16;                       // dab-concurrent.cpp:172-175 warm-up
-        c.stream_off = (int64_t)stream * J.ring * FRAME_SOFT;
-        c.sub_start = J.sub_start[sub];
+        const int64_t cif = J.cif0 + cl;
+        c.valid = cif >= 16;                           // dab-concurrent.cpp:172-175 warm-up
+        c.base = J.src + (int64_t)stream * J.ring * FRAME_SOFT;
+        if (lane < 16) {
+            // element idx of CIF n comes from CIF n - d[idx & 15] (dab-concurrent.cpp:42-43,162-169)
+            const int b = lane;
+            const int rv = ((b & 1) << 3) | ((b & 2) << 1) | ((b & 4) >> 1) | ((b & 8) >> 3);
+            const int64_t g = cif - (15 - rv);
+            int32_t ro = -1;                           // delay line still empty: zeros
+            if (g >= 0) {
+                const int slot = (int)((g >> 2) % J.ring);
+                ro = (slot * NSYM + 3 + 18 * (int)(g & 3)) * SYMBITS + J.sub_start[sub];
+                const Profile &P = J.prof[sub];
+                if (ro < 0 || (int64_t)ro + P.frag > (int64_t)J.ring * FRAME_SOFT) {
+                    atomicOr(J.err, KERR_VITERBI);     // never read outside the stream's ring
+                    ro = -1;
+                }
+            }
+            rowoff[lane] = ro;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (J.valid && !J.valid[c.row]) c.valid = false;
+    if constexpr (KIND != SRC_MSC) {
+        const Profile &P = J.prof[c.prof];
+        const int64_t need = P.nseg ? P.frag : 4 * (int64_t)(P.nbits + 6);
+        const int64_t o = c.base - J.src;
+        if (c.valid && (o < 0 || o + need > J.src_len)) {   // never read outside the buffer
+            if (lane == 0) atomicOr(J.err, KERR_VITERBI);
+            c.valid = false;
+        }
     }
-    if (J.valid && !J.valid[cw]) c.valid = false;
     return c;
 }
 
-// soft value of punctured-input element idx of codeword c
-__device__ __forceinline__ int load_elem(const VitJob &J, const CwInfo &c, int idx) {
-    int64_t off;
-    if (J.kind != SRC_MSC) {
-        off = (c.base - J.src) + idx;
+template <int KIND>
+__device__ __forceinline__ int load_elem(const Src &c, const int32_t *rowoff, int idx) {
+    if constexpr (KIND != SRC_MSC) {
+        return c.base[idx];
     } else {
-        const int64_t g = c.cif - delay16(idx);
-        if (g < 0) return 0;                          // delay lines start at zero
-        const int64_t frame = g >> 2;
-        const int slot = (int)(frame % J.ring);
-        const int64_t loc = ((int64_t)slot * NSYM + 3 + 18 * (int)(g & 3)) * SYMBITS + c.sub_start + idx;
-        if (loc < 0 || loc >= (int64_t)J.ring * FRAME_SOFT) {   // stay inside this stream's ring
-            atomicOr(J.err, KERR_VITERBI);
-            return 0;
-        }
-        off = c.stream_off + loc;
+        const int ro = rowoff[idx & 15];
+        return ro >= 0 ? (int)c.base[ro + idx] : 0;
     }
-    if (off < 0 || off >= J.src_len) {               // never read outside the buffer
-        atomicOr(J.err, KERR_VITERBI);
-        return 0;
-    }
-    return J.src[off];
 }
 
-// the 4 mother-code soft values of trellis step t (positions 4t..4t+3)
-__device__ __forceinline__ void fetch4(const VitJob &J, const CwInfo &c, const Profile *__restrict__ pp, int t, int (&x)[4]) {
+// the 4 mother-code soft values of trellis step t (positions 4t..4t+3), with the
+// depuncturing of deconvolve.cpp:172-237 / fic-handler.cpp:241-270 (0 = erasure)
+template <int KIND>
+__device__ __forceinline__ void fetch4(const Src &c, const int32_t *rowoff, const Profile *__restrict__ pp, int t,
+                                       int (&x)[4]) {
     const Profile &P = *pp;
     const int p = 4 * t;
     if (P.nseg == 0) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) x[e] = load_elem(J, c, p + e);
+        for (int e = 0; e < 4; e++) x[e] = load_elem<KIND>(c, rowoff, p + e);
         return;
     }
     const int blk = p >> 7;
@@ -120,7 +152,7 @@ __device__ __forceinline__ void fetch4(const VitJob &J, const CwInfo &c, const P
     int idx = base + __popc(m & ((1u << b) - 1u));
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-        if ((m >> (b + e)) & 1u) { x[e] = load_elem(J, c, idx); idx++; }
+        if ((m >> (b + e)) & 1u) { x[e] = load_elem<KIND>(c, rowoff, idx); idx++; }
         else x[e] = 0;                               // "a real do not know" (fic-handler.cpp:259)
     }
 }
@@ -134,101 +166,158 @@ struct LaneMask {            // lanes whose bit (5-RHO) is set = lanes holding a
                                 : RHO == 4 ? 0xCCCCCCCCCCCCCCCCull : 0xAAAAAAAAAAAAAAAAull;
 };
 
+// branch metrics of one step for the 8 (b0,b1,b2) output patterns
+// (viterbi.cpp:159-164: metric = sum_j sym_j ^ B_j with b3 = b0)
+__device__ __forceinline__ void put_bm(uint32_t *bm, const int (&s)[4], int lane) {
+    if (lane < VCH) {
+        int y[4];
+#pragma unroll
+        for (int e = 0; e < 4; e++) y[e] = min(max(s[e] + 127, 0), 255);
+#pragma unroll
+        for (int q = 0; q < 8; q++) {
+            const int m0 = (q & 1) ? 255 : 0, m1 = (q & 2) ? 255 : 0, m2 = (q & 4) ? 255 : 0;
+            bm[q * VCH + lane] = (uint32_t)((y[0] ^ m0) + (y[1] ^ m1) + (y[2] ^ m2) + (y[3] ^ m0));
+        }
+    }
+}
+
+// ACS over one tile of nst (<= VCH) trellis steps.  1020 - bm[q] = bm[q ^ 7].
+template <bool FULL>
+__device__ __forceinline__ void acs_tile(const uint32_t *bm, const uint32_t (&off)[6], const uint32_t (&offc)[6],
+                                         uint32_t &x, int lane, int nst, uint64_t *dec) {
+    uint32_t dlo = 0, dhi = 0;
+    sfor<0, VCH / 6>([&](auto gc) {
+        sfor<0, 6>([&](auto rc) {
+            constexpr int rho = decltype(rc)::value;
+            constexpr int j = decltype(gc)::value * 6 + rho;
+            if (FULL || j < nst) {
+                const uint32_t a = x + bm[off[rho] + j];
+                const uint32_t b = xchg<(32 >> rho)>(x, lane) + bm[offc[rho] + j];
+                const uint64_t G = __ballot(a > b), Lt = __ballot(b > a);
+                constexpr uint64_t M = LaneMask<rho>::v;
+                const uint64_t D = (G & ~M) | (Lt & M);
+                dlo = (uint32_t)llvm_amdgcn_writelane((int)(uint32_t)D, j, (int)dlo);
+                dhi = (uint32_t)llvm_amdgcn_writelane((int)(uint32_t)(D >> 32), j, (int)dhi);
+                x = min(a, b);
+            }
+        });
+    });
+    if (FULL ? lane < VCH : lane < nst) dec[lane] = ((uint64_t)dhi << 32) | dlo;
+}
+
+template <int KIND>
 __global__ __launch_bounds__(64) void k_acs(VitJob J) {
     __shared__ uint32_t bm[8 * VCH];
-    const int lane = threadIdx.x, cw = blockIdx.x;
-    const CwInfo c = cw_info(J, cw);
+    __shared__ int32_t rowoff[16];
+    const int lane = threadIdx.x;
+    const Src c = src_of<KIND>(J, xcd_order(blockIdx.x, gridDim.x), rowoff, lane);
     if (!c.valid) return;
     const Profile *pp = J.prof + c.prof;
     const int steps = pp->nbits + 6;
-    uint32_t off[6];
+    uint32_t off[6], offc[6];
 #pragma unroll
     for (int r = 0; r < 6; r++) {
         const int i = rotl6(lane, r) & 31;               // butterfly of the state this lane holds
         const int q = parity((2 * i) & 0155) | (parity((2 * i) & 0117) << 1) | (parity((2 * i) & 0123) << 2);
         off[r] = (uint32_t)(q * VCH);
+        offc[r] = (uint32_t)((q ^ 7) * VCH);
     }
     uint32_t x = lane == 0 ? 0u : 63u;                   // viterbi.cpp:360-371
-    uint64_t *dec = J.dec + (J.dec_off ? J.dec_off[cw] : (int64_t)cw * J.tiles_max * VCH);
-    for (int t0 = 0; t0 < steps; t0 += VCH) {
-        if (lane < VCH && t0 + lane < steps) {
-            int s[4];
-            fetch4(J, c, pp, t0 + lane, s);
-#pragma unroll
-            for (int e = 0; e < 4; e++) s[e] = min(max(s[e] + 127, 0), 255);
-#pragma unroll
-            for (int q = 0; q < 8; q++) {
-                const int m0 = (q & 1) ? 255 : 0, m1 = (q & 2) ? 255 : 0, m2 = (q & 4) ? 255 : 0;
-                bm[q * VCH + lane] = (uint32_t)((s[0] ^ m0) + (s[1] ^ m1) + (s[2] ^ m2) + (s[3] ^ m0));
-            }
-        }
-        const int nst = min(VCH, steps - t0);
-        uint32_t dlo = 0, dhi = 0;
-        sfor<0, VCH / 6>([&](auto gc) {
-            sfor<0, 6>([&](auto rc) {
-                constexpr int rho = decltype(rc)::value;
-                constexpr int j = decltype(gc)::value * 6 + rho;
-                if (j < nst) {
-                    const uint32_t tb = bm[off[rho] + j];
-                    const uint32_t a = x + tb;
-                    const uint32_t xp = xchg<(32 >> rho)>(x, lane);
-                    const uint32_t b = xp + (1020u - tb);
-                    const uint64_t G = __ballot(a > b), Lt = __ballot(b > a);
-                    constexpr uint64_t M = LaneMask<rho>::v;
-                    const uint64_t D = (G & ~M) | (Lt & M);
-                    dlo = (uint32_t)llvm_amdgcn_writelane((int)(uint32_t)D, j, (int)dlo);
-                    dhi = (uint32_t)llvm_amdgcn_writelane((int)(uint32_t)(D >> 32), j, (int)dhi);
-                    x = min(a, b);
-                }
-            });
-        });
-        if (lane < nst) dec[t0 + lane] = ((uint64_t)dhi << 32) | dlo;
+    uint64_t *dec = J.dec + (int64_t)c.row * J.dec_stride;
+    int s[4] = {0, 0, 0, 0};
+    if (lane < VCH && lane < steps) fetch4<KIND>(c, rowoff, pp, lane, s);
+    int t0 = 0;
+    for (; t0 + VCH <= steps; t0 += VCH) {
+        put_bm(bm, s, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        const int tn = t0 + VCH + lane;                  // prefetch the next tile's inputs
+        if (lane < VCH && tn < steps) fetch4<KIND>(c, rowoff, pp, tn, s);
+        acs_tile<true>(bm, off, offc, x, lane, VCH, dec + t0);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    if (t0 < steps) {
+        put_bm(bm, s, lane);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        acs_tile<false>(bm, off, offc, x, lane, steps - t0, dec + t0);
     }
 }
 
+// Chainback (viterbi.cpp:333-357) from state 0, one lane per codeword.  The
+// decision words of a lane are contiguous; TBC-step chunks are loaded one chunk
+// ahead (16-B loads) so the dependent bit walk never waits on memory.
+template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     const int lane = threadIdx.x, cw = blockIdx.x * 64 + lane;
     bool act = cw < J.n_cw;
-    CwInfo c;
-    int N = 0;
+    int N = 0, prof = 0;
     if (act) {
-        c = cw_info(J, cw);
-        act = c.valid;
-        if (act) N = J.prof[c.prof].nbits;
+        // validity and profile by output row (inverse of src_of's mapping)
+        if constexpr (KIND == SRC_MSC) {
+            const int sub = cw % J.nsub;
+            const int cl = (cw / J.nsub) % J.ncif;
+            prof = sub;
+            act = J.cif0 + cl >= 16;
+        } else if constexpr (KIND == SRC_FRAG) {
+            prof = J.cw_prof ? J.cw_prof[cw] : 0;
+        }
+        if (J.valid && !J.valid[cw]) act = false;
+        if (act) N = J.prof[prof].nbits;
     }
     const int steps = act ? N + 6 : 0;
     int tmax = steps;
     for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o));
-    const uint64_t *dec = J.dec + (act ? (J.dec_off ? J.dec_off[cw] : (int64_t)cw * J.tiles_max * VCH) : 0);
+    const uint4 *dq = (const uint4 *)(J.dec + (act ? (int64_t)cw * J.dec_stride : 0));
     uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
     int lr = 0;                                          // lane index holding the traced state
     uint32_t w = 0;
-    int rho = (tmax - 1) % 6;
-    for (int t = tmax - 1; t >= 0; t--) {
-        if (t < steps) {
-            const int p = 5 - rho;
-            const uint64_t D = dec[t];
-            const int u = (lr >> p) & 1;                 // decoded bit of step t
-            const int d = (int)((D >> lr) & 1ull);       // predecessor's msb
-            lr = (lr & ~(1 << p)) | (d << p);
-            if (t < N) {
-                w |= (uint32_t)u << (t & 31);
-                if ((t & 31) == 0) {
-                    if (J.prbs) w ^= J.prbs_words[t >> 5];
-                    if (t + 32 <= N) {
+    const int nch = (tmax + TBC - 1) / TBC;
+    uint4 cur[TBC / 2], nxt[TBC / 2];
+    {
+        const int ch = nch - 1;
+        const bool ld = act && ch * TBC < steps;
 #pragma unroll
-                        for (int k = 0; k < 8; k++) {
-                            const uint32_t nib = (w >> (4 * k)) & 0xFu;
-                            *(uint32_t *)(out + t + 4 * k) = (nib * 0x00204081u) & 0x01010101u;
+        for (int k = 0; k < TBC / 2; k++) cur[k] = ld ? dq[ch * (TBC / 2) + k] : make_uint4(0, 0, 0, 0);
+    }
+    for (int ch = nch - 1; ch >= 0; ch--) {
+        const bool ld = act && ch > 0;
+#pragma unroll
+        for (int k = 0; k < TBC / 2; k++) nxt[k] = ld ? dq[(ch - 1) * (TBC / 2) + k] : make_uint4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = TBC - 1; k >= 0; k--) {
+            const int t = ch * TBC + k;
+            const uint4 q = cur[k >> 1];
+            const uint32_t Dlo = (k & 1) ? q.z : q.x, Dhi = (k & 1) ? q.w : q.y;
+            if (t < steps) {
+                const int p = 5 - (t % 6);
+                const int u = (lr >> p) & 1;                 // decoded bit of step t
+                const int d = (int)(((lr & 32) ? (Dhi >> (lr & 31)) : (Dlo >> lr)) & 1u);   // predecessor's msb
+                lr = (lr & ~(1 << p)) | (d << p);
+                if (t < N) {
+                    w |= (uint32_t)u << (t & 31);
+                    if ((t & 31) == 0) {
+                        if (J.prbs) w ^= J.prbs_words[t >> 5];
+                        if (t + 32 <= N) {
+#pragma unroll
+                            for (int e = 0; e < 8; e++) {
+                                const uint32_t nib = (w >> (4 * e)) & 0xFu;
+                                *(uint32_t *)(out + t + 4 * e) = (nib * 0x00204081u) & 0x01010101u;
+                            }
+                        } else {
+                            for (int i = 0; t + i < N; i++) out[t + i] = (uint8_t)((w >> i) & 1u);
                         }
-                    } else {
-                        for (int i = 0; t + i < N; i++) out[t + i] = (uint8_t)((w >> i) & 1u);
+                        w = 0;
                     }
-                    w = 0;
                 }
             }
         }
-        rho = rho == 0 ? 5 : rho - 1;
+#pragma unroll
+        for (int k = 0; k < TBC / 2; k++) cur[k] = nxt[k];
     }
 }
 
@@ -248,24 +337,31 @@ __global__ void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok,
     ok[f] = r == 0;
 }
 
-hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
-    if (job.n_cw <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_acs, dim3(job.n_cw), dim3(64), 0, st, job);
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_traceback, dim3((job.n_cw + 63) / 64), dim3(64), 0, st, job);
+template <template <int> class K>
+static hipError_t launch_kind(hipStream_t st, const VitJob &job, dim3 grid) {
+    switch (job.kind) {
+    case SRC_MOTHER: hipLaunchKernelGGL(K<SRC_MOTHER>::fn(), grid, dim3(64), 0, st, job); break;
+    case SRC_FRAG:   hipLaunchKernelGGL(K<SRC_FRAG>::fn(), grid, dim3(64), 0, st, job); break;
+    case SRC_FIC:    hipLaunchKernelGGL(K<SRC_FIC>::fn(), grid, dim3(64), 0, st, job); break;
+    case SRC_MSC:    hipLaunchKernelGGL(K<SRC_MSC>::fn(), grid, dim3(64), 0, st, job); break;
+    default: return hipErrorInvalidValue;
+    }
     return hipGetLastError();
 }
+template <int KIND> struct AcsK { static auto fn() { return k_acs<KIND>; } };
+template <int KIND> struct TbK { static auto fn() { return k_traceback<KIND>; } };
 
 hipError_t launch_acs(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_acs, dim3(job.n_cw), dim3(64), 0, st, job);
-    return hipGetLastError();
+    return launch_kind<AcsK>(st, job, dim3(job.n_cw));
 }
 hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_traceback, dim3((job.n_cw + 63) / 64), dim3(64), 0, st, job);
-    return hipGetLastError();
+    return launch_kind<TbK>(st, job, dim3((job.n_cw + 63) / 64));
+}
+hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
+    hipError_t e = launch_acs(st, job);
+    return e != hipSuccess ? e : launch_traceback(st, job);
 }
 
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib) {
