@@ -105,56 +105,95 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
     return c;
 }
 
-template <int KIND>
-__device__ __forceinline__ int load_elem(const Src &c, const int32_t *rowoff, int idx) {
-    if constexpr (KIND != SRC_MSC) {
-        return c.base[idx];
-    } else {
-        const int ro = rowoff[idx & 15];
-        return ro >= 0 ? (int)c.base[ro + idx] : 0;
+// Element offsets (from c.base) of the 4 mother-code soft values of trellis step t
+// (positions 4t..4t+3) with the depuncturing of deconvolve.cpp:172-237 /
+// fic-handler.cpp:241-270.  keep bit e = 0 marks an erasure ("a real do not know",
+// fic-handler.cpp:259, or the zero tail of deconvolve.cpp:182); its offset is a
+// safe in-bounds dummy so the 4 loads can be issued unconditionally.
+// a Profile as wave-uniform registers: only constant indices below, so nothing
+// spills to scratch and nothing goes through the vector memory queue
+struct ProfR {
+    int nbits, nseg, last_end, tail_base;
+    uint32_t mask[4], tail_mask;
+    int blk_end[4], in_base[4];
+};
+__device__ __forceinline__ ProfR prof_regs(const Profile *p) {
+    ProfR r;
+    r.nbits = __builtin_amdgcn_readfirstlane(p->nbits);
+    r.nseg = __builtin_amdgcn_readfirstlane(p->nseg);
+    r.tail_mask = __builtin_amdgcn_readfirstlane(p->tail_mask);
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        r.mask[k] = __builtin_amdgcn_readfirstlane(p->mask[k]);
+        r.blk_end[k] = __builtin_amdgcn_readfirstlane(p->blk_end[k]);
+        r.in_base[k] = __builtin_amdgcn_readfirstlane(p->in_base[k]);
     }
+    r.last_end = 0;
+    r.tail_base = __builtin_amdgcn_readfirstlane(p->in_base[0]);
+#pragma unroll
+    for (int k = 1; k <= 4; k++) {
+        if (r.nseg == k) {
+            r.last_end = r.blk_end[k - 1];
+            r.tail_base = __builtin_amdgcn_readfirstlane(p->in_base[k]);
+        }
+    }
+    return r;
 }
 
-// the 4 mother-code soft values of trellis step t (positions 4t..4t+3), with the
-// depuncturing of deconvolve.cpp:172-237 / fic-handler.cpp:241-270 (0 = erasure)
 template <int KIND>
-__device__ __forceinline__ void fetch4(const Src &c, const int32_t *rowoff, const Profile *__restrict__ pp, int t,
-                                       int (&x)[4]) {
-    const Profile &P = *pp;
+__device__ __forceinline__ uint32_t addr4(const int32_t *rowoff, const ProfR *__restrict__ pp, int t, int (&o)[4]) {
+    const ProfR &P = *pp;
     const int p = 4 * t;
+    uint32_t keep = 0;
+    int idx[4] = {0, 0, 0, 0};
     if (P.nseg == 0) {
 #pragma unroll
-        for (int e = 0; e < 4; e++) x[e] = load_elem<KIND>(c, rowoff, p + e);
-        return;
-    }
-    const int blk = p >> 7;
-    uint32_t m;
-    int base, b;
-    if (blk < P.blk_end[P.nseg - 1]) {
-        int s = 0;
-        while (blk >= P.blk_end[s]) s++;
-        const int bis = blk - (s ? P.blk_end[s - 1] : 0);
-        m = P.mask[s];
-        const int n1 = __popc(m);
-        const int o = p & 127;
-        b = o & 31;
-        base = P.in_base[s] + bis * 4 * n1 + (o >> 5) * n1;
+        for (int e = 0; e < 4; e++) idx[e] = p + e;
+        keep = 0xF;
     } else {
-        b = p - 128 * P.blk_end[P.nseg - 1];
-        if (b >= 24) {                               // beyond PI_X: the memset zeros of the
-#pragma unroll                                       // viterbiBlock (deconvolve.cpp:182)
-            for (int e = 0; e < 4; e++) x[e] = 0;
-            return;
+        const int blk = p >> 7;
+        uint32_t m = 0;
+        int base = 0, b = 0;
+        if (blk < P.last_end) {
+            // segment of this block: selects over the (wave-uniform) profile words,
+            // no per-lane indexing
+            int bs = 0, ib = P.in_base[0];
+            m = P.mask[0];
+#pragma unroll
+            for (int k = 1; k < 4; k++) {
+                if (k < P.nseg && blk >= P.blk_end[k - 1]) { bs = P.blk_end[k - 1]; ib = P.in_base[k]; m = P.mask[k]; }
+            }
+            const int bis = blk - bs;
+            const int n1 = __popc(m);
+            const int oo = p & 127;
+            b = oo & 31;
+            base = ib + bis * 4 * n1 + (oo >> 5) * n1;
+        } else {
+            b = p - 128 * P.last_end;
+            m = b < 24 ? P.tail_mask : 0u;
+            base = P.tail_base;
+            if (b >= 24) b = 0;
         }
-        m = P.tail_mask;
-        base = P.in_base[P.nseg];
+        const uint32_t k4 = (m >> b) & 0xFu;
+        int i = base + __popc(m & ((1u << b) - 1u));
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            idx[e] = i;
+            i += (k4 >> e) & 1;
+        }
+        keep = k4;
     }
-    int idx = base + __popc(m & ((1u << b) - 1u));
 #pragma unroll
     for (int e = 0; e < 4; e++) {
-        if ((m >> (b + e)) & 1u) { x[e] = load_elem<KIND>(c, rowoff, idx); idx++; }
-        else x[e] = 0;                               // "a real do not know" (fic-handler.cpp:259)
+        int off = idx[e];
+        if constexpr (KIND == SRC_MSC) {
+            const int ro = rowoff[idx[e] & 15];
+            if (ro < 0) keep &= ~(1u << e);          // delay line still empty: zero
+            off = ro + idx[e];
+        }
+        o[e] = ((keep >> e) & 1u) ? off : 0;
     }
+    return keep;
 }
 
 __device__ __forceinline__ int parity(int v) { return __popc(v) & 1; }
@@ -166,25 +205,30 @@ struct LaneMask {            // lanes whose bit (5-RHO) is set = lanes holding a
                                 : RHO == 4 ? 0xCCCCCCCCCCCCCCCCull : 0xAAAAAAAAAAAAAAAAull;
 };
 
+// Row stride of the branch-metric table: odd, so the 8 rows that one ACS step
+// reads (8 distinct words, broadcast to 64 lanes) sit in 8 different LDS banks.
+constexpr int BMS = VCH + 1;
+
 // branch metrics of one step for the 8 (b0,b1,b2) output patterns
 // (viterbi.cpp:159-164: metric = sum_j sym_j ^ B_j with b3 = b0)
-__device__ __forceinline__ void put_bm(uint32_t *bm, const int (&s)[4], int lane) {
+__device__ __forceinline__ void put_bm(uint32_t *bm, const int16_t (&s)[4], uint32_t keep, int lane) {
     if (lane < VCH) {
         int y[4];
 #pragma unroll
-        for (int e = 0; e < 4; e++) y[e] = min(max(s[e] + 127, 0), 255);
+        for (int e = 0; e < 4; e++) y[e] = min(max(((keep >> e) & 1u ? (int)s[e] : 0) + 127, 0), 255);
 #pragma unroll
         for (int q = 0; q < 8; q++) {
             const int m0 = (q & 1) ? 255 : 0, m1 = (q & 2) ? 255 : 0, m2 = (q & 4) ? 255 : 0;
-            bm[q * VCH + lane] = (uint32_t)((y[0] ^ m0) + (y[1] ^ m1) + (y[2] ^ m2) + (y[3] ^ m0));
+            bm[q * BMS + lane] = (uint32_t)((y[0] ^ m0) + (y[1] ^ m1) + (y[2] ^ m2) + (y[3] ^ m0));
         }
     }
 }
 
 // ACS over one tile of nst (<= VCH) trellis steps.  1020 - bm[q] = bm[q ^ 7].
+// Returns the tile's decision word of step `lane` (lanes < nst).
 template <bool FULL>
-__device__ __forceinline__ void acs_tile(const uint32_t *bm, const uint32_t (&off)[6], const uint32_t (&offc)[6],
-                                         uint32_t &x, int lane, int nst, uint64_t *dec) {
+__device__ __forceinline__ uint64_t acs_tile(const uint32_t *bm, const uint32_t (&off)[6], const uint32_t (&offc)[6],
+                                             uint32_t &x, int lane, int nst) {
     uint32_t dlo = 0, dhi = 0;
     sfor<0, VCH / 6>([&](auto gc) {
         sfor<0, 6>([&](auto rc) {
@@ -202,49 +246,69 @@ __device__ __forceinline__ void acs_tile(const uint32_t *bm, const uint32_t (&of
             }
         });
     });
-    if (FULL ? lane < VCH : lane < nst) dec[lane] = ((uint64_t)dhi << 32) | dlo;
+    return ((uint64_t)dhi << 32) | dlo;
 }
 
 template <int KIND>
 __global__ __launch_bounds__(64) void k_acs(VitJob J) {
-    __shared__ uint32_t bm[8 * VCH];
+    __shared__ uint32_t bm[8 * BMS];
     __shared__ int32_t rowoff[16];
     const int lane = threadIdx.x;
     const Src c = src_of<KIND>(J, xcd_order(blockIdx.x, gridDim.x), rowoff, lane);
     if (!c.valid) return;
-    const Profile *pp = J.prof + c.prof;
-    const int steps = pp->nbits + 6;
+    // the profile is wave-uniform: scalar loads, kept out of the vector memory queue
+    const ProfR prof = prof_regs(J.prof + c.prof);       // in registers for the whole codeword
+    const ProfR *pp = &prof;
+    const int steps = prof.nbits + 6;
     uint32_t off[6], offc[6];
 #pragma unroll
     for (int r = 0; r < 6; r++) {
         const int i = rotl6(lane, r) & 31;               // butterfly of the state this lane holds
         const int q = parity((2 * i) & 0155) | (parity((2 * i) & 0117) << 1) | (parity((2 * i) & 0123) << 2);
-        off[r] = (uint32_t)(q * VCH);
-        offc[r] = (uint32_t)((q ^ 7) * VCH);
+        off[r] = (uint32_t)(q * BMS);
+        offc[r] = (uint32_t)((q ^ 7) * BMS);
     }
     uint32_t x = lane == 0 ? 0u : 63u;                   // viterbi.cpp:360-371
     uint64_t *dec = J.dec + (int64_t)c.row * J.dec_stride;
-    int s[4] = {0, 0, 0, 0};
-    if (lane < VCH && lane < steps) fetch4<KIND>(c, rowoff, pp, lane, s);
+    // inputs of the next tile are loaded while the current one runs its ACS
+    int16_t s[4];
+    uint32_t keep;
+    auto fetch = [&](int t) {
+        int o[4];
+        keep = 0;
+        if (lane < VCH && t < steps) keep = addr4<KIND>(rowoff, pp, t, o);
+        else o[0] = o[1] = o[2] = o[3] = 0;
+#pragma unroll
+        for (int e = 0; e < 4; e++) s[e] = c.base[o[e]];
+    };
+    // A tile's decisions are stored one tile late, just BEFORE the next prefetch:
+    // vmcnt counts stores too, so the wait for the prefetched inputs then never
+    // has to wait for a store issued after them.
+    fetch(lane);
+    uint64_t dprev = 0;
+    int tprev = -1;
     int t0 = 0;
     for (; t0 + VCH <= steps; t0 += VCH) {
-        put_bm(bm, s, lane);
+        put_bm(bm, s, keep, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const int tn = t0 + VCH + lane;                  // prefetch the next tile's inputs
-        if (lane < VCH && tn < steps) fetch4<KIND>(c, rowoff, pp, tn, s);
-        acs_tile<true>(bm, off, offc, x, lane, VCH, dec + t0);
+        if (tprev >= 0 && lane < VCH) dec[tprev + lane] = dprev;
+        fetch(t0 + VCH + lane);
+        dprev = acs_tile<true>(bm, off, offc, x, lane, VCH);
+        tprev = t0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+    if (tprev >= 0 && lane < VCH) dec[tprev + lane] = dprev;
     if (t0 < steps) {
-        put_bm(bm, s, lane);
+        put_bm(bm, s, keep, lane);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        acs_tile<false>(bm, off, offc, x, lane, steps - t0, dec + t0);
+        const uint64_t d = acs_tile<false>(bm, off, offc, x, lane, steps - t0);
+        if (lane < steps - t0) dec[t0 + lane] = d;
     }
 }
 
