@@ -216,11 +216,11 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, const int16_t (&s)[4], uint
         int y[4];
 #pragma unroll
         for (int e = 0; e < 4; e++) y[e] = min(max(((keep >> e) & 1u ? (int)s[e] : 0) + 127, 0), 255);
+        // y ^ 255 = 255 - y on [0, 255]: 4 partial sums instead of 8 x 4 xors
+        const int a[2] = {y[0] + y[3], 510 - (y[0] + y[3])};
+        const int bc[4] = {y[1] + y[2], 255 - y[1] + y[2], 255 + y[1] - y[2], 510 - (y[1] + y[2])};
 #pragma unroll
-        for (int q = 0; q < 8; q++) {
-            const int m0 = (q & 1) ? 255 : 0, m1 = (q & 2) ? 255 : 0, m2 = (q & 4) ? 255 : 0;
-            bm[q * BMS + lane] = (uint32_t)((y[0] ^ m0) + (y[1] ^ m1) + (y[2] ^ m2) + (y[3] ^ m0));
-        }
+        for (int q = 0; q < 8; q++) bm[q * BMS + lane] = (uint32_t)(a[q & 1] + bc[q >> 1]);
     }
 }
 
@@ -313,10 +313,47 @@ __global__ __launch_bounds__(64) void k_acs(VitJob J) {
 }
 
 // Chainback (viterbi.cpp:333-357) from state 0, one lane per codeword.  The
-// decision words of a lane are contiguous; TBC-step chunks are loaded one chunk
-// ahead (16-B loads) so the dependent bit walk never waits on memory.
+// decision words of a lane are contiguous; TBC-step chunks stream through a
+// 3-deep register ring (two chunks in flight while one is walked), so the
+// dependent bit walk does not wait on memory.
+template <bool CHECK>
+__device__ __forceinline__ void tb_chunk(const uint4 (&c)[TBC / 2], int ch, int steps, int N, int &lr, int &rho,
+                                         bool act, uint8_t *out, const VitJob &J) {
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = TBC - 1; k >= 0; k--) {
+        const int t = ch * TBC + k;
+        const uint32_t Dlo = (k & 1) ? c[k >> 1].z : c[k >> 1].x;
+        const uint32_t Dhi = (k & 1) ? c[k >> 1].w : c[k >> 1].y;
+        const int p = 5 - rho;
+        const int u = (lr >> p) & 1;                                   // decoded bit of step t
+        const uint32_t Dw = (lr & 32) ? Dhi : Dlo;
+        const int d = (int)((Dw >> (lr & 31)) & 1u);                   // predecessor's msb
+        const int nl = (lr & ~(1 << p)) | (d << p);
+        if (!CHECK || t < steps) {
+            lr = nl;
+            w |= (uint32_t)u << k;
+        }
+        rho = rho == 0 ? 5 : rho - 1;
+    }
+    const int t0 = ch * TBC;
+    if (act && t0 < N) {
+        if (J.prbs) w ^= J.prbs_words[t0 >> 5];
+        if (t0 + 32 <= N) {
+#pragma unroll
+            for (int e = 0; e < 8; e++) {
+                const uint32_t nib = (w >> (4 * e)) & 0xFu;
+                *(uint32_t *)(out + t0 + 4 * e) = (nib * 0x00204081u) & 0x01010101u;
+            }
+        } else {
+            for (int i = 0; t0 + i < N; i++) out[t0 + i] = (uint8_t)((w >> i) & 1u);
+        }
+    }
+}
+
 template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
+    static_assert(TBC == 32, "one 32-bit output word per chunk");
     const int lane = threadIdx.x, cw = blockIdx.x * 64 + lane;
     bool act = cw < J.n_cw;
     int N = 0, prof = 0;
@@ -333,55 +370,40 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
         if (J.valid && !J.valid[cw]) act = false;
         if (act) N = J.prof[prof].nbits;
     }
-    const int steps = act ? N + 6 : 0;
-    int tmax = steps;
+    int tmax = act ? N + 6 : 0;
     for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o));
+    if (tmax == 0) return;
+    // inactive lanes walk codeword row 0's decisions (in bounds) and store nothing
+    const int steps = act ? N + 6 : tmax;
+    int smin = steps;
+    for (int o = 32; o > 0; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
     const uint4 *dq = (const uint4 *)(J.dec + (act ? (int64_t)cw * J.dec_stride : 0));
     uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
-    int lr = 0;                                          // lane index holding the traced state
-    uint32_t w = 0;
     const int nch = (tmax + TBC - 1) / TBC;
-    uint4 cur[TBC / 2], nxt[TBC / 2];
-    {
-        const int ch = nch - 1;
-        const bool ld = act && ch * TBC < steps;
+    auto load = [&](uint4 (&c)[TBC / 2], int ch) {
+        const bool ld = ch >= 0;
+        const uint4 *q = dq + (ld ? ch : 0) * (TBC / 2);
 #pragma unroll
-        for (int k = 0; k < TBC / 2; k++) cur[k] = ld ? dq[ch * (TBC / 2) + k] : make_uint4(0, 0, 0, 0);
-    }
-    for (int ch = nch - 1; ch >= 0; ch--) {
-        const bool ld = act && ch > 0;
-#pragma unroll
-        for (int k = 0; k < TBC / 2; k++) nxt[k] = ld ? dq[(ch - 1) * (TBC / 2) + k] : make_uint4(0, 0, 0, 0);
-#pragma unroll
-        for (int k = TBC - 1; k >= 0; k--) {
-            const int t = ch * TBC + k;
-            const uint4 q = cur[k >> 1];
-            const uint32_t Dlo = (k & 1) ? q.z : q.x, Dhi = (k & 1) ? q.w : q.y;
-            if (t < steps) {
-                const int p = 5 - (t % 6);
-                const int u = (lr >> p) & 1;                 // decoded bit of step t
-                const int d = (int)(((lr & 32) ? (Dhi >> (lr & 31)) : (Dlo >> lr)) & 1u);   // predecessor's msb
-                lr = (lr & ~(1 << p)) | (d << p);
-                if (t < N) {
-                    w |= (uint32_t)u << (t & 31);
-                    if ((t & 31) == 0) {
-                        if (J.prbs) w ^= J.prbs_words[t >> 5];
-                        if (t + 32 <= N) {
-#pragma unroll
-                            for (int e = 0; e < 8; e++) {
-                                const uint32_t nib = (w >> (4 * e)) & 0xFu;
-                                *(uint32_t *)(out + t + 4 * e) = (nib * 0x00204081u) & 0x01010101u;
-                            }
-                        } else {
-                            for (int i = 0; t + i < N; i++) out[t + i] = (uint8_t)((w >> i) & 1u);
-                        }
-                        w = 0;
-                    }
-                }
-            }
-        }
-#pragma unroll
-        for (int k = 0; k < TBC / 2; k++) cur[k] = nxt[k];
+        for (int k = 0; k < TBC / 2; k++) c[k] = q[k];
+    };
+    auto walk = [&](const uint4 (&c)[TBC / 2], int ch, int &lr, int &rho) {
+        if ((ch + 1) * TBC <= smin) tb_chunk<false>(c, ch, steps, N, lr, rho, act, out, J);
+        else tb_chunk<true>(c, ch, steps, N, lr, rho, act, out, J);
+    };
+    int lr = 0;                                          // lane index holding the traced state
+    int rho = (nch * TBC - 1) % 6;                       // t mod 6 of the step being walked
+    uint4 A[TBC / 2], B[TBC / 2], C[TBC / 2];
+    load(A, nch - 1);
+    load(B, nch - 2);
+    for (int ch = nch - 1; ch >= 0; ch -= 3) {
+        load(C, ch - 2);
+        walk(A, ch, lr, rho);
+        if (ch < 1) break;
+        load(A, ch - 3);
+        walk(B, ch - 1, lr, rho);
+        if (ch < 2) break;
+        load(B, ch - 4);
+        walk(C, ch - 2, lr, rho);
     }
 }
 
