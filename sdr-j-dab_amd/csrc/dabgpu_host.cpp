@@ -388,10 +388,23 @@ int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n,
     HIPCHK(launch_block0(c->stream, iq, fr, n, c->T, corr, true));
     return 0;
 }
-static const int kChunks = 3;
+// symbols 1..75 of a frame are split over `chunks` waves (each recomputes the FFT
+// of the symbol before its first one): enough waves to fill 256 CUs several
+// times over, at most 25 (3 symbols per wave).
+static const int kMaxChunks = 25;
+static int demod_chunks(int n) {
+    static const int div[] = {3, 5, 15, 25};
+    int c = 3;
+    for (int d : div) {
+        c = d;
+        if ((int64_t)n * d >= 6144) break;
+    }
+    return c;
+}
 static int demod_impl(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t *soft, float *softf,
                       float *fc, bool general) {
     void *part = nullptr;
+    const int kChunks = demod_chunks(n);
     int rc = scratch(c, SC_FC, sizeof(float2) * (size_t)n * kChunks, &part);
     if (rc) return rc;
     HIPCHK(launch_demod(c->stream, iq, fr, n, kChunks, c->T, soft, softf, (float *)part, general));
@@ -652,7 +665,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->si_d, sizeof(int32_t) * SF);
     A((void **)&p->corr_d, sizeof(int16_t) * SF);
     A((void **)&p->fc_d, sizeof(float2) * SF);
-    A((void **)&p->fcpart_d, sizeof(float2) * SF * kChunks);
+    A((void **)&p->fcpart_d, sizeof(float2) * SF * kMaxChunks);
     A((void **)&p->slots_d, sizeof(int32_t) * SF);
     const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
     p->dec_sz = sizeof(uint64_t) * ncw * (size_t)dec_stride_for(p->max_nbits);
@@ -868,6 +881,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     if (n3) {
         HIPCHK(hipMemcpyAsync(p->frames_d, fr3.data(), sizeof(dabgpu_frame) * n3, hipMemcpyHostToDevice, c->stream));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
+        const int kChunks = demod_chunks(n3);
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
