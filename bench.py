@@ -60,6 +60,22 @@ def allreduce_max(dist, x):
     return float(t.item())
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per full-batch launch of `kernel` from the newest committed PMC
+    summary (profiles/rNN_traffic.json, made by tools/pmc_traffic.py from the
+    FETCH_SIZE / WRITE_SIZE passes of this bench command), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_traffic.json")))
+    if not files:
+        return None
+    try:
+        k = json.load(open(files[-1]))["kernels"].get(kernel)
+    except (OSError, ValueError, KeyError):
+        return None
+    return None if k is None else {"bytes": k["hbm_bytes"], "fetch_bytes": k["fetch_bytes"],
+                                   "write_bytes": k["write_bytes"], "source": os.path.basename(files[-1])}
+
+
 def cpu_baseline(frames=2, budget_s=20.0, workers=None):
     """Reference CPU path on the host cores: MSC/FIC depuncture+Viterbi through the
     reference's own compiled viterbi.cpp+spiral-sse.c+deconvolve.cpp (oracle/_ref);
@@ -182,11 +198,12 @@ def main():
     demod_ms = tm["demod"][0]
     demod_bytes = E * F * 75 * (8 * 2552 + 2 * 3072)
     roof_valu = {"kernel": "k_acs (MSC Viterbi)", "bound": "valu", "achieved": acs_ops / (acs_ms * 1e-3) / 1e12,
-                 "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "traffic": None,
+                 "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "traffic": pmc_traffic("dab::k_acs<3>"),
                  "note": "4 int ops per add-compare-select x 64 states per trellis step; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
     roof_valu["frac"] = roof_valu["achieved"] / roof_valu["peak"]
     roof_hbm = {"kernel": "k_demod (FFT+DQPSK)", "bound": "hbm",
-                "achieved": demod_bytes / (demod_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s", "traffic": None,
+                "achieved": demod_bytes / (demod_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "traffic": pmc_traffic("dab::k_demod<false>"), "algorithmic_bytes": demod_bytes,
                 "note": "algorithmic bytes: 8*T_s cf32 in + 2*2K int16 out per data symbol"}
     roof_hbm["frac"] = roof_hbm["achieved"] / roof_hbm["peak"]
     roofline = roof_valu if dom in ("msc_acs", "fic") else roof_hbm
