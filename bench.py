@@ -45,6 +45,11 @@ def dist_setup(n_gpus):
     return rank, local, world, dist
 
 
+def rank_seed0(rank, ensembles):
+    """First ensemble seed of a rank: ranks decode disjoint ensemble sets (weak scaling)."""
+    return 1000 + rank * ensembles
+
+
 def barrier(dist):
     if dist is not None:
         dist.barrier()
@@ -154,7 +159,7 @@ def main():
     total_frames = F * (args.warmup + args.steps + 1) + 1   # +1 step: the profiled pass
     ens = Ensemble(total_frames, subch=C3_SUBCH, snr_db=30.0)
     t0 = time.time()
-    iq = ens.generate_many(E, seed0=1000 + rank * E, threads=min(16, os.cpu_count() or 1))
+    iq = ens.generate_many(E, seed0=rank_seed0(rank, E), threads=min(16, os.cpu_count() or 1))
     gen_s = time.time() - t0
     ctx = dabamd.Context(local)
     diq = ctx.put(iq)
