@@ -63,8 +63,23 @@ typedef struct {
     int16_t bitRate;
     int16_t protLevel;
     int16_t uepFlag;
-    int16_t reserved;
+    int16_t flags;          /* DABGPU_SUBCH_DABPLUS: feed the DAB+ superframe layer */
 } dabgpu_subch;
+#define DABGPU_SUBCH_DABPLUS 1
+
+/* One CIF of one DAB+ subchannel through mp4Processor::addtoFrame
+ * (mp4processor.cpp:107-145) and, when five blocks are buffered and the fire
+ * code holds, processSuperframe (:146-292). */
+typedef struct {
+    int8_t  status;         /* -1 CIF not delivered (de-interleaver warm-up), 0 fewer than 5
+                               blocks buffered, 1 fire code failed, 2 superframe rejected
+                               (RS failure or impossible AU table), 3 superframe decoded */
+    int8_t  num_aus;        /* AUs in the superframe (2, 3, 4 or 6) */
+    int16_t n_corrected;    /* RS symbols corrected (sum over the RSDims codewords) */
+    int16_t au_start[7];    /* au_start[0..num_aus] */
+    uint8_t au_crc_ok;      /* bit i: AU i passed dabPlus_crc */
+    uint8_t reserved;
+} dabgpu_superframe;
 
 /* Per-frame front-end parameters (ofdm-processor.cpp:344-446), one per
  * (stream, frame).  Sample indices are relative to the stream's base.
@@ -149,6 +164,11 @@ int dabgpu_fic_decode_frames(dabgpu_ctx *ctx, const int16_t *softbits_d, const i
  * fragmentSize = length*64 soft bits are given contiguous (already
  * time-de-interleaved), one subchannel description per codeword.
  * Output bits_d[n_cw][24*max_bitRate] (row stride out_stride bytes). */
+/* reedSolomon::dec(rsIn, rsOut, 135) batched (reed-solomon.cpp:129-141; the
+ * RS(255,245) code of mp4processor.cpp:74 shortened to (120,110)): n codewords of
+ * 120 bytes -> 110 corrected bytes each; ret_d[i] = symbols corrected or -1. */
+int dabgpu_rs_decode(dabgpu_ctx *ctx, const uint8_t *in_d, int n, uint8_t *out_d, int16_t *ret_d);
+
 int dabgpu_msc_deconvolve(dabgpu_ctx *ctx, const int16_t *frag_d, int64_t frag_stride,
                           const dabgpu_subch *subch_h, int n_cw, uint8_t *bits_d, int64_t out_stride);
 
@@ -197,6 +217,15 @@ int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride
 int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, const int64_t *n_avail_h,
                     uint8_t *fic_bits_d, uint8_t *fic_crc_d, uint8_t *msc_bits_d, int32_t msc_stride,
                     uint8_t *msc_valid_h);
+/* DAB+ superframe layer for the CIFs of the last dabgpu_pipe_run (call once per
+ * run, after it): mp4Processor::addtoFrame/processSuperframe
+ * (mp4processor.cpp:107-292) for every subchannel flagged DABGPU_SUBCH_DABPLUS,
+ * state (5-CIF byte ring, blockFillIndex, blocksInBuffer) carried across runs.
+ * Outputs (device), DAB+ subchannels numbered in cfg order:
+ *   sf_bytes_d [n_streams][4*n_frames][n_dabplus][sf_stride]: the 110*RSDims
+ *              corrected superframe bytes where info.status == 3
+ *   info_d     [n_streams][4*n_frames][n_dabplus] */
+int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes_d, int32_t sf_stride, dabgpu_superframe *info_d);
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
 /* per-stage kernel time of the last dabgpu_pipe_run (HIP events on the context
  * stream; enabling it adds one stream synchronisation at the end of each run) */
@@ -206,7 +235,8 @@ int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
 #define DABGPU_STAGE_FIC      3   /* FIC Viterbi + CRC                 */
 #define DABGPU_STAGE_MSC_ACS  4   /* MSC Viterbi add-compare-select    */
 #define DABGPU_STAGE_MSC_TB   5   /* MSC chainback + energy dispersal  */
-#define DABGPU_NSTAGE         6
+#define DABGPU_STAGE_DABPLUS  6   /* k_dabplus (superframe, RS, AU CRC) */
+#define DABGPU_NSTAGE         7
 int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on);
 int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms /*[DABGPU_NSTAGE]*/, int32_t *launches /*[DABGPU_NSTAGE] or NULL*/);
 /* device soft-bit ring of the last run ([n_streams][ring][75][3072]) and the slot of

@@ -864,3 +864,31 @@ int orc_superframe(const uint8_t *frame, int base, int bitRate, uint8_t *out, in
     }
     return 1;
 }
+
+void orc_mp4_init(orc_mp4 *m, int bitRate) {                       /* mp4processor.cpp:71-95 */
+    memset(m, 0, sizeof *m);
+    m->bitRate = bitRate;
+}
+
+int orc_mp4_add(orc_mp4 *m, const uint8_t *bits, uint8_t *out, int16_t *n_corrected, int *num_aus,
+                int16_t *au_start, uint8_t *au_crc) {               /* mp4processor.cpp:107-145 */
+    const int nbytes = 3 * m->bitRate;                               /* nbits / 8, nbits = 24 * bitRate */
+    for (int i = 0; i < nbytes; i++) {
+        uint8_t t = 0;
+        for (int j = 0; j < 8; j++) t = (uint8_t)((t << 1) | (bits[8 * i + j] & 1));
+        m->ring[m->fill * nbytes + i] = t;
+    }
+    m->blocks++;
+    m->fill = (m->fill + 1) % 5;
+    *num_aus = 0;
+    *n_corrected = 0;
+    if (m->blocks < 5) return 0;
+    const int base = m->fill * nbytes;
+    if (!orc_firecode_check(&m->ring[base])) { m->blocks = 4; return 1; }
+    if (orc_superframe(m->ring, base, m->bitRate, out, n_corrected, num_aus, au_start, au_crc)) {
+        m->blocks = 0;
+        return 3;
+    }
+    m->blocks = 4;
+    return 2;
+}

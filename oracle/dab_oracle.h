@@ -94,6 +94,19 @@ int     orc_dabplus_crc(const uint8_t *msg, int16_t len);      /* mp4processor.c
 int     orc_superframe(const uint8_t *frame /*[120*RSDims]*/, int base, int bitRate,
                        uint8_t *out, int16_t *n_corrected, int *num_aus, int16_t *au_start, uint8_t *au_crc);
 
+/* mp4Processor::addtoFrame (mp4processor.cpp:107-145): 5-CIF byte ring,
+ * fire-code check at the oldest block, processSuperframe on success.
+ * Returns 0 (fewer than 5 blocks buffered), 1 (fire code failed),
+ * 2 (processSuperframe returned false), 3 (superframe decoded); the
+ * orc_superframe outputs are filled for 2 and 3. */
+typedef struct {
+    int bitRate, fill, blocks;
+    uint8_t ring[120 * 48];
+} orc_mp4;
+void orc_mp4_init(orc_mp4 *m, int bitRate);
+int  orc_mp4_add(orc_mp4 *m, const uint8_t *bits /*[24*bitRate], 1 bit per byte*/, uint8_t *out,
+                 int16_t *n_corrected, int *num_aus, int16_t *au_start, uint8_t *au_crc);
+
 #ifdef __cplusplus
 }
 #endif

@@ -96,6 +96,25 @@ struct VitJob {
     const uint8_t *valid;           // optional per-codeword flag: 0 = skip
 };
 
+// DAB+ superframe layer (k_dabplus.hip)
+constexpr int DP_MAX_RS = 48;       // RSDims = bitRate / 8, bitRate <= 384
+struct DpState {
+    int32_t fill, blocks;           // blockFillIndex, blocksInBuffer (mp4processor.cpp:86-87)
+};
+struct DpJob {
+    const uint8_t *msc;             // MSC bits of the run: [S][ncif][nsub][msc_stride]
+    int32_t msc_stride, ncif, nsub, ndp, nstreams;
+    int64_t cif0;
+    const int32_t *dp_sub;          // [ndp] subchannel index of each DAB+ subchannel
+    const int16_t *dp_br;           // [ndp] its bitRate
+    uint8_t *ring;                  // [S][ndp][120*DP_MAX_RS] 5-CIF byte rings
+    DpState *state;                 // [S][ndp]
+    uint8_t *sf_out;                // [S][ncif][ndp][sf_stride]
+    int64_t sf_stride;
+    dabgpu_superframe *info;        // [S][ncif][ndp]
+    const uint8_t *tabs;            // GF exp[256], log[256], fire-code table uint16[256]
+};
+
 hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
                            int level, int32_t *si, float *mx, float *sm, bool general);
 hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
@@ -109,5 +128,7 @@ hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
 hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
+hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
+hipError_t launch_rs(hipStream_t st, const uint8_t *in, int n, const uint8_t *tabs, uint8_t *out, int16_t *ret);
 
 }  // namespace dab

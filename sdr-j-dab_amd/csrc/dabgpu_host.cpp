@@ -131,7 +131,41 @@ struct HostTables {
             sr[0] = b;
             if (b) prbs_words[i >> 5] |= 1u << (i & 31);
         }
+        // DAB+ tables: GF(2^8) with poly 0435 (galois.cpp:33-63, mp4processor.cpp:74)
+        // and the fire-code syndrome table (firecode-checker.cpp:31-74)
+        dptab.assign(1024, 0);
+        uint8_t *gexp = dptab.data(), *glog = dptab.data() + 256;
+        glog[0] = 255;
+        gexp[255] = 0;
+        for (int i = 0, sr = 1; i < 255; i++) {
+            glog[sr] = (uint8_t)i;
+            gexp[i] = (uint8_t)sr;
+            sr <<= 1;
+            if (sr & 256) sr ^= 0435;
+            sr &= 255;
+        }
+        static const uint8_t fg[16] = {1, 1, 1, 1, 0, 1, 0, 0, 0, 0, 0, 1, 1, 1, 1, 0};
+        uint16_t itab[8];
+        for (int i = 0; i < 8; i++) {
+            uint8_t regs[16] = {};
+            regs[8 + i] = 1;
+            for (int r = 0; r < 8; r++) {
+                const uint8_t z = regs[15];
+                for (int j = 15; j > 0; j--) regs[j] = regs[j - 1] ^ (z & fg[j]);
+                regs[0] = z;
+            }
+            uint16_t v = 0;
+            for (int j = 15; j >= 0; j--) v = (uint16_t)((v << 1) | regs[j]);
+            itab[i] = v;
+        }
+        uint16_t *fire = (uint16_t *)(dptab.data() + 512);
+        for (int i = 0; i < 256; i++) {
+            uint16_t v = 0;
+            for (int j = 0; j < 8; j++) if (i & (1 << j)) v ^= itab[j];
+            fire[i] = v;
+        }
     }
+    std::vector<uint8_t> dptab;             // GF exp[256], log[256], fire uint16[256]
 };
 const HostTables &host_tables() {
     static HostTables t;
@@ -225,6 +259,7 @@ struct dabgpu_ctx {
     float2 *osc = nullptr, *tw = nullptr, *ref_l = nullptr;
     uint32_t *cmap_l = nullptr, *prbs = nullptr;
     float *refarg = nullptr;
+    uint8_t *dptab = nullptr;    // DAB+ tables (HostTables::dptab)
     int32_t *err = nullptr;      // device error word (KERR_* bits)
     OfdmTables T{};
     // growable scratch
@@ -294,7 +329,7 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     int rc = 0;
     if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->tw, t.tw)) || (rc = upload(c, &c->ref_l, t.ref_l)) ||
         (rc = upload(c, &c->cmap_l, t.cmap_l)) || (rc = upload(c, &c->prbs, t.prbs_words)) ||
-        (rc = upload(c, &c->refarg, t.refarg))) {
+        (rc = upload(c, &c->refarg, t.refarg)) || (rc = upload(c, &c->dptab, t.dptab))) {
         dabgpu_ctx_destroy(c);
         return rc;
     }
@@ -317,7 +352,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->cmap_l, (void *)c->prbs,
-                    (void *)c->refarg, (void *)c->err})
+                    (void *)c->refarg, (void *)c->err, (void *)c->dptab})
         if (p) (void)hipFree(p);
     for (auto p : c->scratch) if (p) (void)hipFree(p);
     for (auto e : c->ev) if (e) (void)hipEventDestroy(e);
@@ -587,6 +622,15 @@ struct dabgpu_pipe {
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
     std::vector<int32_t> last_si;
+    // DAB+ superframe layer (mp4Processor per DAB+ subchannel and stream)
+    int NDP = 0, dp_max_rs = 0;
+    int32_t *dp_sub_d = nullptr;
+    int16_t *dp_br_d = nullptr;
+    uint8_t *dp_ring_d = nullptr;     // [S][NDP][120*DP_MAX_RS]
+    DpState *dp_state_d = nullptr;    // [S][NDP]
+    const uint8_t *last_msc = nullptr; // MSC bits of the last successful run
+    int32_t last_msc_stride = 0;
+    int64_t last_cif0 = 0;
     // optional per-stage kernel timing (HIP events on the context stream)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
@@ -622,6 +666,12 @@ inline int32_t lp_after(int32_t lp, int64_t n, int32_t phase) { return modM((int
 }  // namespace
 
 extern "C" {
+
+int dabgpu_rs_decode(dabgpu_ctx *c, const uint8_t *in, int n, uint8_t *out, int16_t *ret) {
+    if (!c || !in || !out || !ret || n < 0) return fail(DABGPU_E_ARG, "bad args");
+    HIPCHK(launch_rs(c->stream, in, n, c->dptab, out, ret));
+    return 0;
+}
 
 int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **out) {
     if (!c || !cfg || !out) return fail(DABGPU_E_ARG, "null arg");
@@ -670,6 +720,32 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
     p->dec_sz = sizeof(uint64_t) * ncw * (size_t)dec_stride_for(p->max_nbits);
     A((void **)&p->dec_d, p->dec_sz);
+    // DAB+ subchannels (mp4Processor: RSDims = bitRate / 8, mp4processor.cpp:83-84)
+    std::vector<int32_t> dps;
+    std::vector<int16_t> dpb;
+    for (int i = 0; i < p->NSUB; i++) {
+        if (!(p->sub[i].flags & DABGPU_SUBCH_DABPLUS)) continue;
+        const int br = p->sub[i].bitRate;
+        if (br < 8 || br % 8 || br / 8 > DP_MAX_RS) {
+            dabgpu_pipe_destroy(p);
+            return fail(DABGPU_E_UNSUP, "DAB+ subchannel %d: bitRate %d is not a multiple of 8 in [8, 384]", i, br);
+        }
+        dps.push_back(i);
+        dpb.push_back((int16_t)br);
+        p->dp_max_rs = std::max(p->dp_max_rs, br / 8);
+    }
+    p->NDP = (int)dps.size();
+    if (p->NDP) {
+        A((void **)&p->dp_sub_d, sizeof(int32_t) * dps.size());
+        A((void **)&p->dp_br_d, sizeof(int16_t) * dpb.size());
+        A((void **)&p->dp_ring_d, (size_t)p->S * p->NDP * 120 * DP_MAX_RS);
+        A((void **)&p->dp_state_d, sizeof(DpState) * (size_t)p->S * p->NDP);
+        if (!rc && (hipMemcpy(p->dp_sub_d, dps.data(), sizeof(int32_t) * dps.size(), hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemcpy(p->dp_br_d, dpb.data(), sizeof(int16_t) * dpb.size(), hipMemcpyHostToDevice) != hipSuccess ||
+                    hipMemset(p->dp_ring_d, 0, (size_t)p->S * p->NDP * 120 * DP_MAX_RS) != hipSuccess ||
+                    hipMemset(p->dp_state_d, 0, sizeof(DpState) * (size_t)p->S * p->NDP) != hipSuccess))
+            rc = fail(DABGPU_E_HIP, "pipe DAB+ init failed");
+    }
     if (!rc) {
         if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(p->substart_d, ss.data(), sizeof(int32_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
@@ -689,7 +765,8 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     (void)hipStreamSynchronize(p->c->stream);
     for (auto e : p->ev_pool) (void)hipEventDestroy(e);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
-                    (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d})
+                    (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d,
+                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
@@ -1029,6 +1106,9 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         HIPCHK(launch_traceback(c->stream, J));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
     }
+    p->last_msc = (msc_bits && p->NSUB > 0 && all) ? msc_bits : nullptr;
+    p->last_msc_stride = msc_stride;
+    p->last_cif0 = cif0;
     if (msc_valid)
         for (int s = 0; s < S; s++)
             for (int q = 0; q < 4 * F; q++) msc_valid[(size_t)s * 4 * F + q] = (all && cif0 + q >= 16) ? 1 : 0;
@@ -1036,16 +1116,6 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         cur[s].cif_count = p->st[s].cif_count + 4 * (int64_t)done[s];
     }
     p->st = cur;
-    if (p->profiling) {
-        HIPCHK(hipStreamSynchronize(c->stream));
-        for (int k = 0; k < DABGPU_NSTAGE; k++) { p->stage_ms[k] = 0.0f; p->stage_n[k] = 0; }
-        for (auto &r : p->ev_rec) {
-            float ms = 0.0f;
-            HIPCHK(hipEventElapsedTime(&ms, p->ev_pool[r.second], p->ev_pool[r.second + 1]));
-            p->stage_ms[r.first] += ms;
-            p->stage_n[r.first] += 1;
-        }
-    }
     if (lost || !all) return fail(DABGPU_E_STATE, "a stream lost sync or ran out of samples (see dabgpu_pipe_state)");
     return 0;
 }
@@ -1057,10 +1127,49 @@ int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on) {
 }
 int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
     if (!p || !ms) return fail(DABGPU_E_ARG, "bad args");
+    // stages recorded since the last dabgpu_pipe_run started (incl. dabgpu_pipe_dabplus)
+    HIPCHK(hipStreamSynchronize(p->c->stream));
+    for (int k = 0; k < DABGPU_NSTAGE; k++) { p->stage_ms[k] = 0.0f; p->stage_n[k] = 0; }
+    for (auto &r : p->ev_rec) {
+        float t = 0.0f;
+        HIPCHK(hipEventElapsedTime(&t, p->ev_pool[r.second], p->ev_pool[r.second + 1]));
+        p->stage_ms[r.first] += t;
+        p->stage_n[r.first] += 1;
+    }
     for (int k = 0; k < DABGPU_NSTAGE; k++) {
         ms[k] = p->stage_ms[k];
         if (launches) launches[k] = p->stage_n[k];
     }
+    return 0;
+}
+
+int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, dabgpu_superframe *info) {
+    if (!p || !sf_bytes || !info) return fail(DABGPU_E_ARG, "null arg");
+    if (p->NDP == 0) return fail(DABGPU_E_STATE, "no DAB+ subchannel in this pipeline");
+    if (!p->last_msc) return fail(DABGPU_E_STATE, "no successful dabgpu_pipe_run with MSC output to consume");
+    if (sf_stride < 110 * p->dp_max_rs) return fail(DABGPU_E_ARG, "sf_stride %d < %d", sf_stride, 110 * p->dp_max_rs);
+    dabgpu_ctx *c = p->c;
+    DpJob J;
+    memset(&J, 0, sizeof J);
+    J.msc = p->last_msc;
+    J.msc_stride = p->last_msc_stride;
+    J.ncif = 4 * p->F;
+    J.nsub = p->NSUB;
+    J.ndp = p->NDP;
+    J.nstreams = p->S;
+    J.cif0 = p->last_cif0;
+    J.dp_sub = p->dp_sub_d;
+    J.dp_br = p->dp_br_d;
+    J.ring = p->dp_ring_d;
+    J.state = p->dp_state_d;
+    J.sf_out = sf_bytes;
+    J.sf_stride = sf_stride;
+    J.info = info;
+    J.tabs = c->dptab;
+    HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, true));
+    HIPCHK(launch_dabplus(c->stream, J));
+    HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, false));
+    p->last_msc = nullptr;                     // each run's CIFs enter the superframe layer once
     return 0;
 }
 

@@ -31,7 +31,18 @@ class DabError(RuntimeError):
 class Subch(C.Structure):
     """audiodata/packetdata subset (dab-constants.h:151-176)."""
     _fields_ = [("startAddr", C.c_int16), ("length", C.c_int16), ("bitRate", C.c_int16),
-                ("protLevel", C.c_int16), ("uepFlag", C.c_int16), ("reserved", C.c_int16)]
+                ("protLevel", C.c_int16), ("uepFlag", C.c_int16), ("flags", C.c_int16)]
+
+
+SUBCH_DABPLUS = 1   # Subch.flags: feed the DAB+ superframe layer
+SUPERFRAME_DTYPE = np.dtype([("status", "i1"), ("num_aus", "i1"), ("n_corrected", "<i2"), ("au_start", "<i2", (7,)),
+                             ("au_crc_ok", "u1"), ("reserved", "u1")])
+
+
+class Superframe(C.Structure):
+    """one CIF of one DAB+ subchannel through mp4Processor (mp4processor.cpp:107-292)"""
+    _fields_ = [("status", C.c_int8), ("num_aus", C.c_int8), ("n_corrected", C.c_int16),
+                ("au_start", C.c_int16 * 7), ("au_crc_ok", C.c_uint8), ("reserved", C.c_uint8)]
 
 
 class Frame(C.Structure):
@@ -80,6 +91,8 @@ def lib() -> C.CDLL:
             "dabgpu_fic_decode": ([vp, vp, i32, vp, vp], i32),
             "dabgpu_fic_decode_frames": ([vp, vp, vp, i32, vp, vp], i32),
             "dabgpu_msc_deconvolve": ([vp, vp, i64, vp, i32, vp, i64], i32),
+            "dabgpu_rs_decode": ([vp, vp, i32, vp, vp], i32),
+            "dabgpu_pipe_dabplus": ([vp, vp, C.c_int32, vp], i32),
             "dabgpu_pipe_create": ([vp, vp, C.POINTER(vp)], i32), "dabgpu_pipe_destroy": ([vp], i32),
             "dabgpu_pipe_acquire": ([vp, vp, i64, vp, vp], i32),
             "dabgpu_pipe_run": ([vp, vp, i64, vp, vp, vp, vp, C.c_int32, vp], i32),
@@ -212,6 +225,18 @@ class Context:
         finally:
             din.free(); dout.free()
 
+    def rs_decode(self, cw: np.ndarray):
+        """reedSolomon::dec(rsIn, rsOut, 135) per row (reed-solomon.cpp:129-141):
+        [n, 120] bytes -> ([n, 110] corrected bytes, [n] symbols corrected or -1)."""
+        cw = np.ascontiguousarray(cw, dtype=np.uint8)
+        n = cw.shape[0]
+        din, dout, dr = self.put(cw), self.buf(max(1, 110 * n)), self.buf(max(2, 2 * n))
+        try:
+            _chk(lib().dabgpu_rs_decode(self.h, din.ptr, n, dout.ptr, dr.ptr), "dabgpu_rs_decode")
+            return dout.download(np.uint8, (n, 110)), dr.download(np.int16, n)
+        finally:
+            din.free(); dout.free(); dr.free()
+
     def prs_sync(self, iq: DevBuf, frames: Sequence[Frame], level: int = 3):
         """phaseReference::findIndex (phasereference.cpp:60-88) per frame window."""
         n = len(frames)
@@ -283,6 +308,12 @@ class Pipeline:
         self.fic_d = ctx.buf(n_streams * n_frames * 4 * 768)
         self.crc_d = ctx.buf(n_streams * n_frames * 12)
         self.msc_d = ctx.buf(max(1, n_streams * 4 * n_frames * len(self.subch) * self.msc_stride))
+        self.dp = [s for s in self.subch if s.flags & SUBCH_DABPLUS]
+        self.sf_stride = max([110 * (s.bitRate // 8) for s in self.dp] + [16])
+        if self.dp:
+            nrec = n_streams * 4 * n_frames * len(self.dp)
+            self.sf_d = ctx.buf(nrec * self.sf_stride)
+            self.sfi_d = ctx.buf(nrec * C.sizeof(Superframe))
 
     def acquire(self, iq: DevBuf, stride: int, start: Sequence[int], n_avail: Sequence[int]) -> None:
         st = np.asarray(start, dtype=np.int64)
@@ -303,7 +334,19 @@ class Pipeline:
             if self.subch else None
         return fic, crc, msc, valid
 
-    STAGES = ("prs_sync", "block0", "demod", "fic", "msc_acs", "msc_traceback")
+    def dabplus(self, download: bool = True):
+        """DAB+ superframe layer over the CIFs of the last run() (mp4processor.cpp:107-292).
+        Returns (info [S, 4F, n_dabplus] Superframe records, bytes [S, 4F, n_dabplus, sf_stride])."""
+        _chk(lib().dabgpu_pipe_dabplus(self.h, self.sf_d.ptr, self.sf_stride, self.sfi_d.ptr), "dabgpu_pipe_dabplus")
+        if not download:
+            return None
+        nd = len(self.dp)
+        raw = self.sfi_d.download(np.uint8, self.S * 4 * self.F * nd * C.sizeof(Superframe))
+        info = np.frombuffer(raw.tobytes(), dtype=SUPERFRAME_DTYPE).reshape(self.S, 4 * self.F, nd)
+        sf = self.sf_d.download(np.uint8, (self.S, 4 * self.F, nd, self.sf_stride))
+        return info, sf
+
+    STAGES = ("prs_sync", "block0", "demod", "fic", "msc_acs", "msc_traceback", "dabplus")
 
     def set_profiling(self, on: bool = True) -> None:
         _chk(lib().dabgpu_pipe_set_profiling(self.h, 1 if on else 0), "set_profiling")
@@ -337,7 +380,7 @@ class Pipeline:
 
     def close(self) -> None:
         if self.h:
-            for b in (self.fic_d, self.crc_d, self.msc_d):
+            for b in (self.fic_d, self.crc_d, self.msc_d) + ((self.sf_d, self.sfi_d) if self.dp else ()):
                 b.free()
             lib().dabgpu_pipe_destroy(self.h)
             self.h = None

@@ -346,7 +346,9 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
         std::vector<uint8_t> info(nb), mother(4 * (nb + 6)), punct(frag_len[s] + 64);
         int rsdims = sc.bitRate / 8;
         std::vector<uint8_t> sf(120 * std::max(rsdims, 1));
-        int sf_pos = 0;
+        // dabplus = 1 + k: the superframe grid is shifted by k CIFs (k = 1..4 makes the
+        // receiver's first five CIFs straddle two superframes)
+        int sf_pos = sc.dabplus > 1 ? ((sc.dabplus - 1) % 5) * (nb / 8) : 0;
         for (int e = -19; e < 4 * F; e++) {
             if (sc.dabplus) {
                 // 5 CIFs carry one superframe; superframes start at e = -19 + 5m

@@ -27,7 +27,7 @@ typedef struct {
     int16_t bitRate;     /* kbit/s */
     int16_t protLevel;   /* UEP level 1..5, or EEP 0100|lvl (A) / 0200|lvl (B) */
     int16_t uep;         /* 1 = UEP (uepFlag 0 in the reference), 0 = EEP */
-    int16_t dabplus;     /* 1: payload is a DAB+ superframe stream with valid RS/fire code */
+    int16_t dabplus;     /* 1+k: DAB+ superframe stream (valid RS/fire code/AU CRCs), grid shifted by k CIFs */
 } dabsynth_subch;
 
 typedef struct {

@@ -98,3 +98,36 @@ def find_index(win, level=3):
     mx, sm = C.c_float(), C.c_float()
     r = oracle().orc_find_index(P(np.ascontiguousarray(win, np.float32)), level, C.byref(mx), C.byref(sm))
     return r, mx.value, sm.value
+
+
+def rs_dec(cw):
+    """reedSolomon::dec(rsIn, rsOut, 135) (reed-solomon.cpp:129-141): (out[110], ret)."""
+    out = np.zeros(110, np.uint8)
+    r = oracle().orc_rs_dec(P(np.ascontiguousarray(cw, np.uint8)), P(out))
+    return out, int(r)
+
+
+class MP4:
+    """mp4Processor::addtoFrame state machine (mp4processor.cpp:107-292) over
+    successive CIF payloads of one DAB+ subchannel."""
+
+    class _St(C.Structure):
+        _fields_ = [("bitRate", C.c_int), ("fill", C.c_int), ("blocks", C.c_int), ("ring", C.c_uint8 * (120 * 48))]
+
+    def __init__(self, bitrate):
+        self.st = MP4._St()
+        self.br = bitrate
+        oracle().orc_mp4_init(C.byref(self.st), bitrate)
+
+    def add(self, bits):
+        """-> dict(status, out[110*RSDims], n_corrected, num_aus, au_start, au_crc)"""
+        rs = self.br // 8
+        out = np.zeros(110 * rs, np.uint8)
+        nc = C.c_int16(0)
+        na = C.c_int(0)
+        aus = np.zeros(8, np.int16)
+        crc = np.zeros(8, np.uint8)
+        st = oracle().orc_mp4_add(C.byref(self.st), P(np.ascontiguousarray(bits, np.uint8)), P(out),
+                                  C.byref(nc), C.byref(na), P(aus), P(crc))
+        return dict(status=int(st), out=out, n_corrected=int(nc.value), num_aus=int(na.value),
+                    au_start=aus, au_crc=crc)

@@ -121,6 +121,25 @@ def test_oracle_dabplus_superframe():
     assert good >= 2
 
 
+def test_oracle_mp4_state_machine():
+    """mp4Processor::addtoFrame (mp4processor.cpp:107-145): with the superframe grid
+    shifted by 2 CIFs the fire code fails until the ring is aligned, then every
+    fifth CIF completes a superframe whose bytes are the transmitted ones."""
+    from dabamd.synth import Ensemble
+    e = Ensemble(8, subch=[(0, 48, 64, 0o103, 0, 3)], snr_db=300.0)
+    g = e.generate(5)
+    m = orc.MP4(64)
+    st = []
+    for n in range(16, 32):
+        r = m.add(g["msc"][n, 0, :24 * 64])
+        st.append(r["status"])
+        if r["status"] == 3:
+            sf = np.packbits(g["msc"][n - 4:n + 1, 0, :24 * 64].reshape(-1))
+            assert np.array_equal(r["out"], sf[:110 * 8])
+            assert r["num_aus"] == 4 and r["au_crc"][:4].all() and r["n_corrected"] == 0
+    assert st == [0, 0, 0, 0, 1, 1, 1, 3, 0, 0, 0, 0, 3, 0, 0, 0]
+
+
 def test_abi_library_exports_every_declared_symbol():
     hdr = open(os.path.join(ROOT, "include", "dabgpu.h")).read()
     names = set(re.findall(r"\b(dabgpu_[a-z0-9_]+)\s*\(", hdr))
