@@ -27,6 +27,13 @@ RT_SYMBOLS = 76 / 0.096            # symbols/s of one real-time Mode-I ensemble 
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 C3_SUBCH = [(96 * i, 96, 128, 3, 1, 0) for i in range(9)]   # (startAddr, CUs, kbps, level, uep, dab+)
+# C5: 16 ensembles x 16 DAB+ subchannels (64 kbit/s EEP-3A, 48 CUs, RSDims 8) = 256
+C5_SUBCH = [(48 * i, 48, 64, 0o103, 0, 1) for i in range(16)]
+WORKLOADS = {
+    "c3": (C3_SUBCH, 64, "C3: 64 concurrent Mode-I ensembles/GPU, FIC + full MSC (9 x UEP-3 128 kbps)"),
+    "c5": (C5_SUBCH, 16, "C5: 256 DAB+ subchannels/GPU (16 ensembles x 16 x 64 kbps EEP-3A), FIC + MSC Viterbi "
+                         "+ superframe sync + RS(120,110) + AU CRC"),
+}
 
 
 def dist_setup(n_gpus):
@@ -81,7 +88,7 @@ def pmc_traffic(kernel):
                                    "write_bytes": k["write_bytes"], "source": os.path.basename(files[-1])}
 
 
-def cpu_baseline(frames=2, budget_s=20.0, workers=None):
+def cpu_baseline(frames=2, budget_s=20.0, workers=None, workload="c3"):
     """Reference CPU path on the host cores: MSC/FIC depuncture+Viterbi through the
     reference's own compiled viterbi.cpp+spiral-sse.c+deconvolve.cpp (oracle/_ref);
     OFDM front end through the oracle's C restatement (FFTW3f absent).  One worker
@@ -90,7 +97,7 @@ def cpu_baseline(frames=2, budget_s=20.0, workers=None):
     workers = workers or min(16, os.cpu_count() or 1)
     ctx = mp.get_context("fork")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_cpu_worker, args=(w, frames, budget_s, q)) for w in range(workers)]
+    procs = [ctx.Process(target=_cpu_worker, args=(w, frames, budget_s, q, workload)) for w in range(workers)]
     for p in procs:
         p.start()
     res = [q.get() for _ in procs]
@@ -102,13 +109,13 @@ def cpu_baseline(frames=2, budget_s=20.0, workers=None):
     return syms / secs, workers, kind, syms
 
 
-def _cpu_worker(w, frames, budget_s, q):
-    import ctypes as C
+def _cpu_worker(w, frames, budget_s, q, workload="c3"):
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_py as orc
     from dabamd.synth import Ensemble
     ref = orc.ref()
-    e = Ensemble(frames + 4, subch=C3_SUBCH, snr_db=300.0)
+    subch = WORKLOADS[workload][0]
+    e = Ensemble(frames + 4, subch=subch, snr_db=300.0)
     g = e.generate(9000 + w, truth=False)
     prbs = orc.prbs(3072)
     t0 = time.perf_counter()
@@ -120,15 +127,21 @@ def _cpu_worker(w, frames, budget_s, q):
             fic = soft[f, 0:3].reshape(-1)
             for b in range(4):
                 orc.fic_process(fic[2304 * b:2304 * (b + 1)])
+        mp4 = [orc.MP4(sc[2]) if sc[5] else None for sc in subch]
         for c in range(4 * n):
-            for (sa, ln, br, pl, uep, _) in C3_SUBCH:
+            for k, (sa, ln, br, pl, uep, dp) in enumerate(subch):
                 frag = np.ascontiguousarray(cifs[c, sa * 64:(sa + ln) * 64])
+                out = np.zeros(24 * br, np.uint8)
                 if ref is not None:
-                    out = np.zeros(24 * br, np.uint8)
-                    ref.ref_uep_deconvolve(br, pl, orc.P(frag), len(frag), orc.P(out))
-                    out ^= prbs
+                    if uep:
+                        ref.ref_uep_deconvolve(br, pl, orc.P(frag), len(frag), orc.P(out))
+                    else:
+                        ref.ref_eep_deconvolve(br, pl, orc.P(frag), len(frag), orc.P(out))
+                    out ^= prbs[:24 * br]
                 else:
-                    orc.msc_deconvolve(1, br, pl, frag)
+                    out = orc.msc_deconvolve(uep, br, pl, frag)
+                if mp4[k] is not None:
+                    mp4[k].add(out)
         done += n * 76
         el = time.perf_counter() - t0
         if el >= budget_s:
@@ -141,7 +154,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--ensembles", type=int, default=64, help="ensembles per GPU (C3: 64)")
+    ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
+    ap.add_argument("--ensembles", type=int, default=0, help="ensembles per GPU (default: C3 64, C5 16)")
     ap.add_argument("--frames", type=int, default=8, help="frames per ensemble per step")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
@@ -151,13 +165,15 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before this process touches the GPU: the workers are forked children
-        cpu = cpu_baseline(budget_s=args.cpu_seconds)
+        cpu = cpu_baseline(budget_s=args.cpu_seconds, workload=args.workload)
     import dabamd
     from dabamd.synth import Ensemble
 
-    E, F = args.ensembles, args.frames
+    SUBCH, E_default, wl_desc = WORKLOADS[args.workload]
+    dabplus = any(s[5] for s in SUBCH)
+    E, F = args.ensembles or E_default, args.frames
     total_frames = F * (args.warmup + args.steps + 1) + 1   # +1 step: the profiled pass
-    ens = Ensemble(total_frames, subch=C3_SUBCH, snr_db=30.0)
+    ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0)
     t0 = time.time()
     iq = ens.generate_many(E, seed0=rank_seed0(rank, E), threads=min(16, os.cpu_count() or 1))
     gen_s = time.time() - t0
@@ -165,19 +181,26 @@ def main():
     diq = ctx.put(iq)
     del iq
     stride = ens.length
-    subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0, 0) for s in C3_SUBCH]
+    subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, dabamd.SUBCH_DABPLUS if s[5] else 0)
+            for s in SUBCH]
     pipe = dabamd.Pipeline(ctx, E, F, subs)
     pipe.acquire(diq, stride, [0] * E, [stride] * E)
     n_avail = [stride] * E
 
+    def step(download=False):
+        r = pipe.run(diq, stride, n_avail, download=download)
+        if dabplus:
+            return r, pipe.dabplus(download=download)
+        return r, None
+
     for _ in range(args.warmup):
-        pipe.run(diq, stride, n_avail, download=False)
+        step()
     ctx.sync()
     barrier(dist)
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        pipe.run(diq, stride, n_avail, download=False)
+        step()
     ctx.sync()
     el = time.perf_counter() - t0
     barrier(dist)
@@ -185,9 +208,15 @@ def main():
 
     # one extra profiled step (outside the timed region): per-kernel HIP-event times
     pipe.set_profiling(True)
-    fic, crc, msc, valid = pipe.run(diq, stride, n_avail, download=True)
+    (fic, crc, msc, valid), dp = step(download=True)
     tm = pipe.timing()
     crc_ok = float(crc.mean())
+    sf_ok = None
+    if dp is not None:
+        info = dp[0]
+        sf_ok = {"superframes": int((info["status"] == 3).sum()),
+                 "au_crc_pass": int(sum(bin(int(x)).count("1") for x in info["au_crc_ok"][info["status"] == 3])),
+                 "cif_records": int((info["status"] >= 0).sum())}
     pipe.set_profiling(False)
 
     symbols = world * E * F * 76 * args.steps
@@ -196,10 +225,9 @@ def main():
         return
     # dominant kernel + its roofline
     dom = max(tm, key=lambda k: tm[k][0])
-    steps_per_cw = 24 * 128 + 6
-    n_msc_cw = E * 4 * F * len(C3_SUBCH)
+    acs_steps = E * 4 * F * sum(24 * s[2] + 6 for s in SUBCH)
     acs_ms = tm["msc_acs"][0]
-    acs_ops = n_msc_cw * steps_per_cw * 64 * 4      # 2 adds + compare + select per ACS
+    acs_ops = acs_steps * 64 * 4                    # 2 adds + compare + select per ACS
     demod_ms = tm["demod"][0]
     demod_bytes = E * F * 75 * (8 * 2552 + 2 * 3072)
     roof_valu = {"kernel": "k_acs (MSC Viterbi)", "bound": "valu", "achieved": acs_ops / (acs_ms * 1e-3) / 1e12,
@@ -219,22 +247,24 @@ def main():
         "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32+u32",
         "data": "synthetic (dabsynth transmitter, 30 dB SNR)",
-        "config": {"workload": "C3: 64 concurrent Mode-I ensembles/GPU, FIC + full MSC (9 x UEP-3 128 kbps)",
+        "config": {"workload": wl_desc,
                    "ensembles_per_gpu": E, "frames_per_step": F, "parallelism": f"ensemble-shard x{world}"},
         "realtime_ensembles_per_gpu": value / world / RT_SYMBOLS,
         "roofline": roofline,
         "roofline_hbm_demod": roof_hbm,
         "kernel_ms_per_step": {k: v[0] for k, v in tm.items()},
         "fic_crc_pass_rate": crc_ok,
+        "dabplus_last_step": sf_ok,
         "gen_seconds": gen_s,
     }
     if cpu is not None:
         v, cores, kind, syms = cpu
         out["cpu_baseline"] = {"value": v, "unit": "symbols/s", "cores": cores, "kind": kind,
-                               "sample": f"{cores} workers x own synthetic C3 ensemble (6 frames, 9 UEP-3 128k "
-                                         f"subch), ~{args.cpu_seconds:.0f}s each, {syms} symbols total; "
-                                         "Viterbi/depuncture = reference viterbi.cpp+spiral-sse.c+deconvolve.cpp, "
-                                         "OFDM = oracle C restatement (FFTW3f absent)"}
+                               "sample": f"{cores} workers x own synthetic {args.workload.upper()} ensemble "
+                                         f"(6 frames, {len(SUBCH)} subch), ~{args.cpu_seconds:.0f}s each, {syms} "
+                                         "symbols total; Viterbi/depuncture = reference viterbi.cpp+spiral-sse.c+"
+                                         "deconvolve.cpp, OFDM (and DAB+ RS/superframe) = oracle C restatement "
+                                         "(FFTW3f absent)"}
     print(json.dumps(out))
 
 
