@@ -98,6 +98,7 @@ struct VitJob {
 
 // DAB+ superframe layer (k_dabplus.hip)
 constexpr int DP_MAX_RS = 48;       // RSDims = bitRate / 8, bitRate <= 384
+constexpr int DP_TAB_BYTES = 256 + 256 + 512 + 2560 + 512;   // GF exp/log, fire, mul[10], crc
 struct DpState {
     int32_t fill, blocks;           // blockFillIndex, blocksInBuffer (mp4processor.cpp:86-87)
 };
@@ -112,7 +113,7 @@ struct DpJob {
     uint8_t *sf_out;                // [S][ncif][ndp][sf_stride]
     int64_t sf_stride;
     dabgpu_superframe *info;        // [S][ncif][ndp]
-    const uint8_t *tabs;            // GF exp[256], log[256], fire-code table uint16[256]
+    const uint8_t *tabs;            // DP_TAB_BYTES: GF exp, log, fire table, alpha^i multiply, CRC
 };
 
 hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,

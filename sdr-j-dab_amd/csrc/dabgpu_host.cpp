@@ -133,7 +133,7 @@ struct HostTables {
         }
         // DAB+ tables: GF(2^8) with poly 0435 (galois.cpp:33-63, mp4processor.cpp:74)
         // and the fire-code syndrome table (firecode-checker.cpp:31-74)
-        dptab.assign(1024, 0);
+        dptab.assign(DP_TAB_BYTES, 0);
         uint8_t *gexp = dptab.data(), *glog = dptab.data() + 256;
         glog[0] = 255;
         gexp[255] = 0;
@@ -163,6 +163,15 @@ struct HostTables {
             uint16_t v = 0;
             for (int j = 0; j < 8; j++) if (i & (1 << j)) v ^= itab[j];
             fire[i] = v;
+        }
+        uint8_t *mul = dptab.data() + 1024;            // mul[i][s] = s * alpha^i
+        for (int i = 0; i < 10; i++)
+            for (int v = 0; v < 256; v++) mul[i * 256 + v] = v ? gexp[(glog[v] + i) % 255] : 0;
+        uint16_t *crc = (uint16_t *)(dptab.data() + 1024 + 2560);   // CRC-CCITT, msb first
+        for (int b = 0; b < 256; b++) {
+            uint32_t c = (uint32_t)b << 8;
+            for (int k = 0; k < 8; k++) c = (c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1);
+            crc[b] = (uint16_t)(c & 0xFFFFu);
         }
     }
     std::vector<uint8_t> dptab;             // GF exp[256], log[256], fire uint16[256]

@@ -23,8 +23,11 @@ __device__ __forceinline__ int mod255(int x) { return x % 255; }
 struct GfTabs {
     uint8_t exp[256];
     uint8_t log[256];
-    uint16_t fire[256];
+    uint16_t fire[256];      // fire-code syndrome table
+    uint8_t mul[10][256];    // s * alpha^i: one lookup per Horner step of syndrome i
+    uint16_t crc[256];       // CRC-CCITT (0x1021, msb first) byte table
 };
+static_assert(sizeof(GfTabs) == DP_TAB_BYTES, "host table layout");
 
 __device__ __forceinline__ int gmul(const GfTabs &g, int a, int b) {
     return (a && b) ? g.exp[mod255(g.log[a] + g.log[b])] : 0;
@@ -33,21 +36,26 @@ __device__ __forceinline__ int gdiv(const GfTabs &g, int a, int b) {
     return a ? g.exp[mod255(RS_NN + g.log[a] - g.log[b])] : 0;
 }
 
-// reedSolomon::dec (reed-solomon.cpp:129-141 with cutlen 135, decode_rs :143-399)
-// on the 120 code bytes d[0..119] (full-codeword position 135 + m); corrects d in
-// place and returns the number of corrected symbols, or -1.
-__device__ int rs_decode_lane(uint8_t *d, const GfTabs &g, uint8_t *roots, uint8_t *locs) {
-    int syn[10];
-#pragma unroll
-    for (int i = 0; i < 10; i++) syn[i] = 0;
-    for (int m = 0; m < 120; m++) {                       // Horner over the codeword (:231-266)
-        const int v = d[m * 1];
-#pragma unroll
-        for (int i = 0; i < 10; i++) {
-            const int s = syn[i];
-            syn[i] = v ^ (s ? g.exp[mod255(g.log[s] + i)] : 0);
-        }
+// Syndrome i of a codeword whose byte m (m = 0..119, full-codeword position
+// 135 + m; the 135 leading pad bytes are zero and leave the Horner sum at zero)
+// is at src[m * step] (reed-solomon.cpp:231-266).
+__device__ __forceinline__ int rs_syndrome(const uint8_t *src, int step, int wrap, int start, int i, const GfTabs &g) {
+    int s = 0, o = start;
+    for (int m = 0; m < 120; m++) {
+        s = src[o] ^ g.mul[i][s];
+        o += step;
+        if (o >= wrap) o -= wrap;
     }
+    return s;
+}
+
+// decode_rs after the syndromes (reed-solomon.cpp:268-399): Berlekamp-Massey,
+// Chien search over all 255 positions, error evaluator, Forney.  Returns the
+// number of corrected symbols or -1, and the corrections to apply: fix_pos[k]
+// (full-codeword position) ^= fix_val[k] for k < *nfix.
+__device__ int rs_solve(const int (&syn)[10], const GfTabs &g, uint8_t *roots, uint8_t *locs, uint8_t *fix_pos,
+                        uint8_t *fix_val, int *nfix) {
+    *nfix = 0;
     int any = 0;
 #pragma unroll
     for (int i = 0; i < 10; i++) any |= syn[i];
@@ -123,6 +131,7 @@ __device__ int rs_decode_lane(uint8_t *d, const GfTabs &g, uint8_t *roots, uint8
     }
     // Forney (:183-227)
     const int dmax = (deg < 9 ? deg : 9) & ~1;
+    int nf = 0;
     for (int jj = count - 1; jj >= 0; jj--) {
         const int r = roots[jj], loc = locs[jj];
         int num1 = 0;
@@ -134,17 +143,23 @@ __device__ int rs_decode_lane(uint8_t *d, const GfTabs &g, uint8_t *roots, uint8
 #pragma unroll
         for (int i = 0; i <= 8; i += 2)
             if (i <= dmax && LL[i + 1] != RS_NN) den ^= g.exp[mod255(LL[i + 1] + (i ? (i * r) % RS_NN : 0))];
-        if (den == 0) return -1;
+        if (den == 0) {
+            *nfix = nf;                                  // corrections made before the failure stay
+            return -1;
+        }
         if (num1 != 0) {
             if (loc >= RS_NN - 10) {
                 count--;
             } else {
                 int c = mod255(g.log[num1] + g.log[num2]);
                 c = mod255(c + RS_NN - g.log[den]);
-                if (loc >= RS_PAD) d[loc - RS_PAD] ^= g.exp[c];
+                fix_pos[nf] = (uint8_t)loc;
+                fix_val[nf] = g.exp[c];
+                nf++;
             }
         }
     }
+    *nfix = nf;
     return count;
 }
 
@@ -160,15 +175,11 @@ __device__ bool fire_ok(const uint8_t *x, const GfTabs &g) {
 }
 
 // dabPlus_crc (mp4processor.cpp:40-61)
-__device__ bool au_crc_ok(const uint8_t *msg, int len, int limit) {
+__device__ bool au_crc_ok(const uint8_t *msg, int len, int limit, const GfTabs &g) {
     uint32_t acc = 0xFFFF;
-    for (int i = 0; i < len; i++) {
-        uint32_t data = (uint32_t)(i < limit ? msg[i] : 0) << 8;
-        for (int j = 0; j < 8; j++) {
-            acc = ((data ^ acc) & 0x8000u) ? ((acc << 1) ^ 0x1021u) & 0xFFFFu : (acc << 1) & 0xFFFFu;
-            data = (data << 1) & 0xFFFFu;
-        }
-    }
+    const int n = len < limit ? len : limit;
+    for (int i = 0; i < n; i++) acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ msg[i]) & 0xFFu]) & 0xFFFFu;
+    for (int i = n; i < len; i++) acc = ((acc << 8) ^ g.crc[(acc >> 8) & 0xFFu]) & 0xFFFFu;
     const uint32_t hi = len < limit ? msg[len] : 0, lo = len + 1 < limit ? msg[len + 1] : 0;
     const uint32_t crc = ~((hi << 8) | lo) & 0xFFFFu;
     return (crc ^ acc) == 0;
@@ -184,8 +195,8 @@ __global__ __launch_bounds__(64) void k_dabplus(DpJob J) {
     __shared__ GfTabs g;
     __shared__ uint8_t ring[120 * DP_MAX_RS];
     __shared__ uint8_t outv[110 * DP_MAX_RS + 16];
-    __shared__ uint8_t rows[DP_MAX_RS * RS_ROW];
-    __shared__ uint8_t rl[64 * 20];
+    __shared__ int16_t syn_s[10 * DP_MAX_RS];
+    __shared__ uint8_t rl[64 * 40];
     __shared__ int32_t red[64];
     const int lane = threadIdx.x;
     const int stream = blockIdx.x / J.ndp, dp = blockIdx.x % J.ndp;
@@ -230,13 +241,31 @@ __global__ __launch_bounds__(64) void k_dabplus(DpJob J) {
                 info.status = 1;
                 st.blocks = 4;
             } else {
-                // processSuperframe: RS over the RSDims interleaved columns (:165-179)
+                // processSuperframe: RS over the RSDims interleaved columns (:165-179).
+                // Byte k of column j is ring[(base + j + k*RS) % fsz], so the
+                // uncorrected output outv[j + k*RS] is the ring rotated by base.
+                for (int i = lane; i < 110 * RS; i += 64) {
+                    const int o = base + i;
+                    outv[i] = ring[o < fsz ? o : o - fsz];
+                }
+                // syndromes: every (column, root) pair is one Horner chain on one lane
+                for (int p = lane; p < 10 * RS; p += 64) {
+                    const int j = p / 10, i = p - 10 * j;
+                    syn_s[p] = (int16_t)rs_syndrome(ring, RS, fsz, base + j < fsz ? base + j : base + j - fsz, i, g);
+                }
+                wave_sync();
                 int ler = 0;
-                if (lane < RS) {
-                    uint8_t *row = rows + lane * RS_ROW;
-                    for (int k = 0; k < 120; k++) row[k] = ring[(base + lane + k * RS) % fsz];
-                    ler = rs_decode_lane(row, g, rl + lane * 20, rl + lane * 20 + 10);
-                    for (int k = 0; k < 110; k++) outv[lane + k * RS] = row[k];
+                if (lane < RS) {                                 // one column per lane
+                    int sy[10];
+#pragma unroll
+                    for (int i = 0; i < 10; i++) sy[i] = syn_s[10 * lane + i];
+                    uint8_t *w = rl + lane * 40;
+                    int nf = 0;
+                    ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
+                    for (int f = 0; f < nf; f++) {
+                        const int m = w[20 + f] - RS_PAD;
+                        if (m >= 0 && m < 110) outv[lane + m * RS] ^= w[30 + f];
+                    }
                 }
                 red[lane] = ler;
                 wave_sync();
@@ -278,7 +307,7 @@ __global__ __launch_bounds__(64) void k_dabplus(DpJob J) {
                         int ai = 0, an = 0;
                         for (int i = 0; i < 7; i++) if (i == lane) { ai = a[i]; an = a[i + 1]; }
                         const int len = an - ai - 2;
-                        mine = au_crc_ok(outv + ai, len, end - ai) ? 1 : 0;
+                        mine = au_crc_ok(outv + ai, len, end - ai, g) ? 1 : 0;
                     }
                     const uint64_t crcmask = __ballot(mine);
                     info.au_crc_ok = (uint8_t)(crcmask & 0x3F);
@@ -314,14 +343,23 @@ __global__ __launch_bounds__(64) void k_rs(const uint8_t *__restrict__ in, int n
                                           uint8_t *__restrict__ out, int16_t *__restrict__ ret) {
     __shared__ GfTabs g;
     __shared__ uint8_t rows[64 * RS_ROW];
-    __shared__ uint8_t rl[64 * 20];
+    __shared__ uint8_t rl[64 * 40];
     const int lane = threadIdx.x, cw = blockIdx.x * 64 + lane;
     for (int i = lane; i < (int)sizeof(GfTabs); i += 64) ((uint8_t *)&g)[i] = tabs[i];
     wave_sync();
     if (cw >= n) return;
     uint8_t *row = rows + lane * RS_ROW;
     for (int k = 0; k < 120; k++) row[k] = in[(int64_t)cw * 120 + k];
-    const int r = rs_decode_lane(row, g, rl + lane * 20, rl + lane * 20 + 10);
+    int sy[10];
+#pragma unroll
+    for (int i = 0; i < 10; i++) sy[i] = rs_syndrome(row, 1, 1 << 30, 0, i, g);
+    uint8_t *w = rl + lane * 40;
+    int nf = 0;
+    const int r = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
+    for (int f = 0; f < nf; f++) {
+        const int m = w[20 + f] - RS_PAD;
+        if (m >= 0) row[m] ^= w[30 + f];
+    }
     for (int k = 0; k < 110; k++) out[(int64_t)cw * 110 + k] = row[k];
     ret[cw] = (int16_t)r;
 }
