@@ -66,6 +66,8 @@ typedef struct {
     int16_t flags;          /* DABGPU_SUBCH_DABPLUS: feed the DAB+ superframe layer */
 } dabgpu_subch;
 #define DABGPU_SUBCH_DABPLUS 1
+#define DABGPU_SUBCH_RAW     2   /* dabgpu_msc_deconvolve: no energy dispersal (the bare
+                                    uep_/eep_deconvolve::deconvolve output) */
 
 /* One CIF of one DAB+ subchannel through mp4Processor::addtoFrame
  * (mp4processor.cpp:107-145) and, when five blocks are buffered and the fire
@@ -160,7 +162,7 @@ int dabgpu_fic_decode_frames(dabgpu_ctx *ctx, const int16_t *softbits_d, const i
                              int n_frames, uint8_t *bits_d, uint8_t *crc_ok_d);
 
 /* uep_/eep_deconvolve::deconvolve + energy dispersal (deconvolve.cpp:172-237,
- * 325-366; dab-concurrent.cpp:183-190) for n_cw codewords whose
+ * 325-366; dab-concurrent.cpp:183-190; no dispersal with DABGPU_SUBCH_RAW) for n_cw codewords whose
  * fragmentSize = length*64 soft bits are given contiguous (already
  * time-de-interleaved), one subchannel description per codeword.
  * Output bits_d[n_cw][24*max_bitRate] (row stride out_stride bytes). */

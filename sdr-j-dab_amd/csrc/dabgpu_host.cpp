@@ -557,7 +557,10 @@ int dabgpu_msc_deconvolve(dabgpu_ctx *c, const int16_t *frag, int64_t frag_strid
     std::vector<Profile> profs;
     std::vector<int32_t> cwp(n_cw);
     int maxbits = 8;
+    const int raw = n_cw ? (sub[0].flags & DABGPU_SUBCH_RAW) : 0;
     for (int i = 0; i < n_cw; i++) {
+        if ((sub[i].flags & DABGPU_SUBCH_RAW) != raw)
+            return fail(DABGPU_E_ARG, "DABGPU_SUBCH_RAW must be the same for every codeword of a call");
         Profile p;
         int rc = make_profile(sub[i], p);
         if (rc) return fail(DABGPU_E_UNSUP, "subchannel %d: protection (uep=%d, level 0%o, %d kbps) undefined",
@@ -588,7 +591,7 @@ int dabgpu_msc_deconvolve(dabgpu_ctx *c, const int16_t *frag, int64_t frag_strid
     J.cw_prof = (const int32_t *)cd;
     J.out = bits;
     J.out_stride = out_stride;
-    J.prbs = 1;
+    J.prbs = raw ? 0 : 1;
     if ((rc = run_viterbi(c, J, maxbits))) return rc;
     return kernel_errors(c);
 }

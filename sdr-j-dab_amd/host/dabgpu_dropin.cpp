@@ -1,0 +1,298 @@
+// dabgpu_dropin.cpp -- see dabgpu_dropin.h.  Every class is a thin host shell over
+// the C ABI: buffers are allocated once per object, each call is one upload, one
+// (or a few) kernel launches and one download on the thread's HIP stream.
+#include "dabgpu_dropin.h"
+
+#include <cstring>
+#include <memory>
+#include <string>
+
+namespace dabgpu {
+
+namespace {
+int g_device = 0;
+
+struct ctx_holder {
+    dabgpu_ctx *c = nullptr;
+    ~ctx_holder() {
+        if (c) dabgpu_ctx_destroy(c);
+    }
+};
+thread_local ctx_holder t_ctx;
+
+void chk(int rc, const char *what) {
+    if (rc != DABGPU_OK) throw error(rc, std::string(what) + ": " + dabgpu_last_error());
+}
+}  // namespace
+
+void set_device(int device) { g_device = device; }
+
+dabgpu_ctx *thread_context() {
+    if (!t_ctx.c) chk(dabgpu_ctx_create(g_device, &t_ctx.c), "dabgpu_ctx_create");
+    return t_ctx.c;
+}
+
+devbuf::~devbuf() {
+    if (p_ && t_ctx.c) dabgpu_free(t_ctx.c, p_);
+}
+
+void devbuf::resize(size_t bytes) {
+    if (bytes <= n_) return;
+    dabgpu_ctx *c = thread_context();
+    if (p_) dabgpu_free(c, p_);
+    p_ = nullptr;
+    n_ = 0;
+    chk(dabgpu_alloc(c, bytes, &p_), "dabgpu_alloc");
+    n_ = bytes;
+}
+
+void devbuf::upload(const void *h, size_t bytes) {
+    resize(bytes);
+    chk(dabgpu_memcpy_h2d(thread_context(), p_, h, bytes), "dabgpu_memcpy_h2d");
+}
+
+void devbuf::download(void *h, size_t bytes) const {
+    chk(dabgpu_memcpy_d2h(thread_context(), h, p_, bytes), "dabgpu_memcpy_d2h");
+}
+
+// ---- viterbi family --------------------------------------------------------
+viterbi::viterbi(int16_t wordlength) : wordlength_(wordlength) {
+    in_.resize(sizeof(int16_t) * 4 * (wordlength + 6));
+    out_.resize(wordlength + 16);
+}
+
+void viterbi::deconvolve(int16_t *input, uint8_t *output) {
+    in_.upload(input, sizeof(int16_t) * 4 * (wordlength_ + 6));
+    chk(dabgpu_viterbi(thread_context(), (const int16_t *)in_.get(), 1, wordlength_, (uint8_t *)out_.get()),
+        "dabgpu_viterbi");
+    out_.download(output, wordlength_);
+}
+
+namespace {
+bool msc_one(const dabgpu_subch &sub, devbuf &in, devbuf &out, int16_t *v, int32_t size, uint8_t *outBuffer) {
+    const int nbits = 24 * sub.bitRate;
+    in.upload(v, sizeof(int16_t) * size);
+    const int rc = dabgpu_msc_deconvolve(thread_context(), (const int16_t *)in.get(), size, &sub, 1,
+                                         (uint8_t *)out.get(), nbits);
+    if (rc == DABGPU_E_UNSUP || rc == DABGPU_E_ARG) return false;   // profile undefined / fragment too short
+    chk(rc, "dabgpu_msc_deconvolve");
+    out.download(outBuffer, nbits);
+    return true;
+}
+}  // namespace
+
+uep_deconvolve::uep_deconvolve(int16_t bitRate, int16_t protLevel) : viterbi(24 * bitRate) {
+    sub_ = dabgpu_subch{0, 0, bitRate, protLevel, 0, DABGPU_SUBCH_RAW};
+}
+
+bool uep_deconvolve::deconvolve(int16_t *v, int32_t size, uint8_t *outBuffer) {
+    return msc_one(sub_, in_, out_, v, size, outBuffer);
+}
+
+eep_deconvolve::eep_deconvolve(int16_t bitRate, int16_t protLevel) : viterbi(24 * bitRate) {
+    sub_ = dabgpu_subch{0, 0, bitRate, protLevel, 1, DABGPU_SUBCH_RAW};
+}
+
+bool eep_deconvolve::deconvolve(int16_t *v, int32_t size, uint8_t *outBuffer) {
+    return msc_one(sub_, in_, out_, v, size, outBuffer);
+}
+
+// ---- reedSolomon -------------------------------------------------------------
+reedSolomon::reedSolomon(uint16_t symsize, uint16_t gfpoly, uint16_t fcr, uint16_t prim, uint16_t nroots) {
+    if (symsize != 8 || gfpoly != 0435 || fcr != 0 || prim != 1 || nroots != 10)
+        throw error(DABGPU_E_UNSUP, "reedSolomon: only the DAB+ code (8, 0435, 0, 1, 10) runs on the GPU");
+    in_.resize(120);
+    out_.resize(112);
+    ret_.resize(16);
+}
+
+int16_t reedSolomon::dec(const uint8_t *data_in, uint8_t *data_out, int16_t cutlen) {
+    if (cutlen != 135) throw error(DABGPU_E_UNSUP, "reedSolomon::dec: only cutlen 135 (RS(120,110))");
+    in_.upload(data_in, 120);
+    chk(dabgpu_rs_decode(thread_context(), (const uint8_t *)in_.get(), 1, (uint8_t *)out_.get(), (int16_t *)ret_.get()),
+        "dabgpu_rs_decode");
+    int16_t r = 0;
+    out_.download(data_out, 110);
+    ret_.download(&r, sizeof r);
+    return r;
+}
+
+// ---- phaseReference ------------------------------------------------------------
+phaseReference::phaseReference(int16_t threshold) : threshold_(threshold) {
+    iq_.resize(sizeof(float) * 2 * DABGPU_TU);
+    fr_.resize(sizeof(dabgpu_frame));
+    si_.resize(16);
+}
+
+int32_t phaseReference::findIndex(DSPCOMPLEX *v) {
+    iq_.upload(v, sizeof(float) * 2 * DABGPU_TU);
+    dabgpu_frame f;
+    std::memset(&f, 0, sizeof f);
+    f.n_samples = DABGPU_TU;                      // samples already mixed: NCO phase 0
+    fr_.upload(&f, sizeof f);
+    chk(dabgpu_prs_sync(thread_context(), (const float *)iq_.get(), (const dabgpu_frame *)fr_.get(), 1, threshold_,
+                        (int32_t *)si_.get(), nullptr, nullptr),
+        "dabgpu_prs_sync");
+    int32_t r = 0;
+    si_.download(&r, sizeof r);
+    return r;
+}
+
+// ---- ficHandler -------------------------------------------------------------------
+ficHandler::ficHandler(fib_cb cb, int16_t bitsperBlock) : cb_(std::move(cb)), ofdm_input_(2304) {
+    if (bitsperBlock != 2 * DABGPU_K) throw error(DABGPU_E_UNSUP, "ficHandler: Mode I (3072 bits per block) only");
+    in_.resize(sizeof(int16_t) * 2304);
+    bits_.resize(768);
+    crc_.resize(16);
+}
+
+void ficHandler::process_ficBlock(int16_t *data, int16_t blkno) {   // fic-handler.cpp:192-224
+    if (blkno == 1) {
+        index_ = 0;
+        ficno_ = 0;
+    }
+    for (int i = 0; i < 2 * DABGPU_K; i++) {
+        ofdm_input_[index_++] = data[i];
+        if (index_ >= 2304) {
+            // process_ficInput (fic-handler.cpp:241-321) on the GPU
+            in_.upload(ofdm_input_.data(), sizeof(int16_t) * 2304);
+            chk(dabgpu_fic_decode(thread_context(), (const int16_t *)in_.get(), 1, (uint8_t *)bits_.get(),
+                                  (uint8_t *)crc_.get()),
+                "dabgpu_fic_decode");
+            uint8_t bits[768], ok[3];
+            bits_.download(bits, 768);
+            crc_.download(ok, 3);
+            for (int k = 0; k < 3; k++) {
+                total_++;
+                good_ += ok[k] ? 1 : 0;
+                if (cb_) cb_(bits + 256 * k, ok[k] != 0, (int16_t)ficno_);
+            }
+            index_ = 0;
+            ficno_++;
+        }
+    }
+}
+
+int16_t ficHandler::get_ficRatio() const { return total_ ? (int16_t)(100 * good_ / total_) : 0; }
+
+// ---- ensembleDecoder -------------------------------------------------------------
+ensembleDecoder::ensembleDecoder(const config &cfg) : cfg_(cfg) {
+    dabgpu_pipe_cfg pc;
+    std::memset(&pc, 0, sizeof pc);
+    pc.n_streams = cfg.n_streams;
+    pc.n_frames = cfg.n_frames;
+    pc.n_subch = (int32_t)cfg.subch.size();
+    pc.threshold = cfg.threshold;
+    pc.freq_sync_method = 1;
+    pc.subch = cfg.subch.data();
+    chk(dabgpu_pipe_create(thread_context(), &pc, &pipe_), "dabgpu_pipe_create");
+    int maxbits = 768, maxrs = 0;
+    for (size_t i = 0; i < cfg.subch.size(); i++) {
+        maxbits = std::max(maxbits, 24 * (int)cfg.subch[i].bitRate);
+        if (cfg.subch[i].flags & DABGPU_SUBCH_DABPLUS) {
+            dp_index_.push_back((int)i);
+            maxrs = std::max(maxrs, cfg.subch[i].bitRate / 8);
+        }
+    }
+    ndp_ = (int)dp_index_.size();
+    msc_stride_ = (maxbits + 15) / 16 * 16;
+    sf_stride_ = std::max(16, 110 * maxrs);
+    const size_t SF = (size_t)cfg.n_streams * cfg.n_frames;
+    fic_.resize(SF * 4 * 768);
+    crc_.resize(SF * 12);
+    msc_.resize(std::max<size_t>(1, SF * 4 * cfg.subch.size() * msc_stride_));
+    if (ndp_) {
+        sf_.resize(SF * 4 * ndp_ * sf_stride_);
+        sfi_.resize(SF * 4 * ndp_ * sizeof(dabgpu_superframe));
+    }
+}
+
+ensembleDecoder::~ensembleDecoder() {
+    if (pipe_) dabgpu_pipe_destroy(pipe_);
+}
+
+void ensembleDecoder::load(const std::vector<const DSPCOMPLEX *> &samples, const std::vector<int64_t> &n) {
+    if ((int)samples.size() != cfg_.n_streams || (int)n.size() != cfg_.n_streams)
+        throw error(DABGPU_E_ARG, "ensembleDecoder::load: one sample array per stream");
+    stride_ = 0;
+    for (int64_t k : n) stride_ = std::max(stride_, k);
+    iq_.resize(sizeof(float) * 2 * (size_t)stride_ * cfg_.n_streams);
+    for (int s = 0; s < cfg_.n_streams; s++)
+        chk(dabgpu_memcpy_h2d(thread_context(), (float *)iq_.get() + 2 * stride_ * s, samples[s],
+                              sizeof(float) * 2 * n[s]),
+            "dabgpu_memcpy_h2d");
+    navail_ = n;
+    frames_done_ = 0;
+}
+
+void ensembleDecoder::acquire() {
+    std::vector<int64_t> start(cfg_.n_streams, 0);
+    chk(dabgpu_pipe_acquire(pipe_, (const float *)iq_.get(), stride_, start.data(), navail_.data()),
+        "dabgpu_pipe_acquire");
+}
+
+bool ensembleDecoder::step() {
+    const int S = cfg_.n_streams, F = cfg_.n_frames, NS = (int)cfg_.subch.size();
+    std::vector<uint8_t> valid((size_t)S * 4 * F);
+    const int rc = dabgpu_pipe_run(pipe_, (const float *)iq_.get(), stride_, navail_.data(), (uint8_t *)fic_.get(),
+                                   (uint8_t *)crc_.get(), NS ? (uint8_t *)msc_.get() : nullptr, msc_stride_,
+                                   valid.data());
+    if (rc != DABGPU_OK && rc != DABGPU_E_STATE) chk(rc, "dabgpu_pipe_run");
+    const bool ok = rc == DABGPU_OK;
+    // frames committed per stream: FIC is delivered for those, MSC only on success
+    std::vector<dabgpu_frame> fr((size_t)S * F);
+    std::vector<int32_t> si((size_t)S * F);
+    chk(dabgpu_pipe_frames(pipe_, fr.data(), si.data()), "dabgpu_pipe_frames");
+    std::vector<uint8_t> fic((size_t)S * F * 4 * 768), crc((size_t)S * F * 12);
+    fic_.download(fic.data(), fic.size());
+    crc_.download(crc.data(), crc.size());
+    for (int s = 0; s < S && fib_cb_; s++)
+        for (int f = 0; f < F; f++) {
+            if (fr[(size_t)s * F + f].window == 0) continue;   // not committed in this run
+            for (int b = 0; b < 4; b++)
+                for (int k = 0; k < 3; k++) {
+                    const size_t o = (((size_t)s * F + f) * 4 + b) * 768 + 256 * k;
+                    fib_cb_(s, frames_done_ + f, b, fic.data() + o, crc[((size_t)s * F + f) * 12 + 3 * b + k] != 0);
+                }
+        }
+    if (ok && NS && msc_cb_) {
+        std::vector<uint8_t> msc((size_t)S * 4 * F * NS * msc_stride_);
+        msc_.download(msc.data(), msc.size());
+        for (int s = 0; s < S; s++)
+            for (int c = 0; c < 4 * F; c++) {
+                if (!valid[(size_t)s * 4 * F + c]) continue;
+                for (int k = 0; k < NS; k++)
+                    msc_cb_(s, 4 * frames_done_ + c, k, msc.data() + (((size_t)s * 4 * F + c) * NS + k) * msc_stride_,
+                         24 * cfg_.subch[k].bitRate);
+            }
+    }
+    if (ok && ndp_) {
+        chk(dabgpu_pipe_dabplus(pipe_, (uint8_t *)sf_.get(), sf_stride_, (dabgpu_superframe *)sfi_.get()),
+            "dabgpu_pipe_dabplus");
+        if (sf_cb_) {
+            std::vector<dabgpu_superframe> info((size_t)S * 4 * F * ndp_);
+            std::vector<uint8_t> bytes(info.size() * sf_stride_);
+            sfi_.download(info.data(), info.size() * sizeof(dabgpu_superframe));
+            sf_.download(bytes.data(), bytes.size());
+            for (size_t r = 0; r < info.size(); r++) {
+                if (info[r].status < 0) continue;
+                const int d = (int)(r % ndp_);
+                const int c = (int)((r / ndp_) % (4 * F));
+                const int s = (int)(r / ndp_ / (4 * F));
+                const int k = dp_index_[d];
+                sf_cb_(s, 4 * frames_done_ + c, k, info[r], bytes.data() + r * sf_stride_,
+                    info[r].status == 3 ? 110 * (cfg_.subch[k].bitRate / 8) : 0);
+            }
+        }
+    }
+    if (ok) frames_done_ += F;
+    return ok;
+}
+
+dabgpu_stream_state ensembleDecoder::state(int stream) const {
+    dabgpu_stream_state st;
+    chk(dabgpu_pipe_state(pipe_, stream, &st), "dabgpu_pipe_state");
+    return st;
+}
+
+}  // namespace dabgpu
