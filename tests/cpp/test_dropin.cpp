@@ -54,7 +54,7 @@ int main() {
     }
     // uep / eep deconvolve (deconvolve.cpp:142-366), no energy dispersal
     {
-        struct Case { int uep, br, pl, cus; } cases[] = {{1, 128, 3, 96}, {1, 64, 2, 56}, {0, 64, 0103, 48},
+        struct Case { int uep, br, pl, cus; } cases[] = {{1, 128, 3, 96}, {1, 64, 2, 58}, {0, 64, 0103, 48},
                                                          {0, 96, 0204, 54}};
         for (auto &cs : cases) {
             const int frag = cs.cus * 64;
