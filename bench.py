@@ -195,13 +195,13 @@ def main():
 
     for _ in range(args.warmup):
         step()
-    ctx.sync()
+    pipe.sync()
     barrier(dist)
-    ctx.sync()
+    pipe.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
-    ctx.sync()
+    pipe.sync()
     el = time.perf_counter() - t0
     barrier(dist)
     el = allreduce_max(dist, el)

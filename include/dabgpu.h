@@ -229,6 +229,11 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, co
  *   info_d     [n_streams][4*n_frames][n_dabplus] */
 int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes_d, int32_t sf_stride, dabgpu_superframe *info_d);
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
+/* Wait until everything the pipeline enqueued is done.  The FIC/MSC/DAB+ outputs
+ * of a run are written by the pipeline's own HIP stream (overlapping the next
+ * run's OFDM front end): call this before reading them.  Also reports a kernel
+ * that refused out-of-bounds work (DABGPU_E_BOUNDS). */
+int dabgpu_pipe_sync(dabgpu_pipe *p);
 /* per-stage kernel time of the last dabgpu_pipe_run (HIP events on the context
  * stream; enabling it adds one stream synchronisation at the end of each run) */
 #define DABGPU_STAGE_PRS      0   /* k_prs_sync   (findIndex)          */

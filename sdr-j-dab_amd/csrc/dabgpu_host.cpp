@@ -643,7 +643,15 @@ struct dabgpu_pipe {
     const uint8_t *last_msc = nullptr; // MSC bits of the last successful run
     int32_t last_msc_stride = 0;
     int64_t last_cif0 = 0;
-    // optional per-stage kernel timing (HIP events on the context stream)
+    // channel decoding (FIC/MSC Viterbi, DAB+) runs on its own stream so run r's
+    // back end overlaps run r+1's front end; the ring holds 2F+4 frames per
+    // stream so run r+1's demod never overwrites a slot run r's MSC reads.
+    hipStream_t vs = nullptr;
+    hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr};
+    bool back_rec[2] = {false, false};
+    int64_t run_idx = 0;
+    Profile *ficprof_d = nullptr;
+    // optional per-stage kernel timing (HIP events on the stage's stream)
     bool profiling = false;
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<int, int>> ev_rec;   // (stage, index of start event; end = +1)
@@ -653,6 +661,7 @@ struct dabgpu_pipe {
 
 static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
     if (!p->profiling) return hipSuccess;
+    hipStream_t st = (stage >= DABGPU_STAGE_FIC) ? p->vs : p->c->stream;
     if (start) {
         size_t need = 2 * (p->ev_rec.size() + 1);
         while (p->ev_pool.size() < need) {
@@ -663,9 +672,9 @@ static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
         }
         int idx = (int)(2 * p->ev_rec.size());
         p->ev_rec.push_back({stage, idx});
-        return hipEventRecord(p->ev_pool[idx], p->c->stream);
+        return hipEventRecord(p->ev_pool[idx], st);
     }
-    return hipEventRecord(p->ev_pool[p->ev_rec.back().second + 1], p->c->stream);
+    return hipEventRecord(p->ev_pool[p->ev_rec.back().second + 1], st);
 }
 
 namespace {
@@ -695,7 +704,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     p->S = cfg->n_streams;
     p->F = cfg->n_frames;
     p->NSUB = cfg->n_subch;
-    p->R = cfg->n_frames + 4;
+    p->R = 2 * cfg->n_frames + 4;
     p->threshold = cfg->threshold;
     p->sub.assign(cfg->subch, cfg->subch + cfg->n_subch);
     p->st.assign(p->S, StreamSt());
@@ -732,6 +741,17 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
     p->dec_sz = sizeof(uint64_t) * ncw * (size_t)dec_stride_for(p->max_nbits);
     A((void **)&p->dec_d, p->dec_sz);
+    A((void **)&p->ficprof_d, sizeof(Profile));
+    if (!rc && (hipStreamCreateWithFlags(&p->vs, hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_front, hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_back[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_back[1], hipEventDisableTiming) != hipSuccess))
+        rc = fail(DABGPU_E_HIP, "pipe stream/event create failed");
+    if (!rc) {
+        const Profile fp = fic_profile();
+        if (hipMemcpy(p->ficprof_d, &fp, sizeof fp, hipMemcpyHostToDevice) != hipSuccess)
+            rc = fail(DABGPU_E_HIP, "pipe FIC profile upload failed");
+    }
     // DAB+ subchannels (mp4Processor: RSDims = bitRate / 8, mp4processor.cpp:83-84)
     std::vector<int32_t> dps;
     std::vector<int16_t> dpb;
@@ -775,7 +795,12 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
 int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     if (!p) return 0;
     (void)hipStreamSynchronize(p->c->stream);
+    if (p->vs) (void)hipStreamSynchronize(p->vs);
     for (auto e : p->ev_pool) (void)hipEventDestroy(e);
+    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1]})
+        if (e) (void)hipEventDestroy(e);
+    if (p->vs) (void)hipStreamDestroy(p->vs);
+    if (p->ficprof_d) (void)hipFree(p->ficprof_d);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d})
@@ -1044,6 +1069,10 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     p->last_frames.assign((size_t)S * F, dabgpu_frame());
     p->last_si.assign((size_t)S * F, 0);
     p->ev_rec.clear();
+    // at most one run of overlap: run r-2's channel decoding must be done before
+    // this run's demod reuses its ring slots
+    const int par = (int)(p->run_idx & 1);
+    if (p->back_rec[par]) HIPCHK(hipStreamWaitEvent(c->stream, p->ev_back[par], 0));
     std::vector<int> done(S, 0);
     std::vector<StreamSt> cur = p->st;
     bool lost = false;
@@ -1055,18 +1084,17 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     }
     bool all = true;
     for (int s = 0; s < S; s++) if (done[s] != F) all = false;
+    // channel decoding on the pipeline's stream, after this run's front end
+    HIPCHK(hipEventRecord(p->ev_front, c->stream));
+    HIPCHK(hipStreamWaitEvent(p->vs, p->ev_front, 0));
     // FIC for every committed frame
     {
         std::vector<int32_t> slots((size_t)S * F);
         for (int s = 0; s < S; s++)
             for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = p->last_frames[(size_t)s * F + f].out_slot;
         if (fic_bits) {
-            HIPCHK(hipMemcpyAsync(p->slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, c->stream));
-            Profile pf = fic_profile();
-            void *pd = nullptr;
-            int rc = scratch(c, SC_PROF, sizeof pf, &pd);
-            if (rc) return rc;
-            HIPCHK(hipMemcpyAsync(pd, &pf, sizeof pf, hipMemcpyHostToDevice, c->stream));
+            HIPCHK(hipMemcpyAsync(p->slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, p->vs));
+            void *pd = p->ficprof_d;
             VitJob J;
             memset(&J, 0, sizeof J);
             J.kind = SRC_FIC;
@@ -1083,8 +1111,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             J.dec = p->dec_d;
             J.dec_stride = dec_stride_for(768);
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-            HIPCHK(launch_viterbi(c->stream, J));
-            if (fic_crc) HIPCHK(launch_fic_post(c->stream, fic_bits, fic_crc, 12 * S * F));
+            HIPCHK(launch_viterbi(p->vs, J));
+            if (fic_crc) HIPCHK(launch_fic_post(p->vs, fic_bits, fic_crc, 12 * S * F));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         }
     }
@@ -1112,12 +1140,15 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         J.dec = p->dec_d;
         J.dec_stride = dec_stride_for(p->max_nbits);
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs(c->stream, J));
+        HIPCHK(launch_acs(p->vs, J));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
-        HIPCHK(launch_traceback(c->stream, J));
+        HIPCHK(launch_traceback(p->vs, J));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
     }
+    HIPCHK(hipEventRecord(p->ev_back[par], p->vs));
+    p->back_rec[par] = true;
+    p->run_idx++;
     p->last_msc = (msc_bits && p->NSUB > 0 && all) ? msc_bits : nullptr;
     p->last_msc_stride = msc_stride;
     p->last_cif0 = cif0;
@@ -1141,6 +1172,7 @@ int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
     if (!p || !ms) return fail(DABGPU_E_ARG, "bad args");
     // stages recorded since the last dabgpu_pipe_run started (incl. dabgpu_pipe_dabplus)
     HIPCHK(hipStreamSynchronize(p->c->stream));
+    HIPCHK(hipStreamSynchronize(p->vs));
     for (int k = 0; k < DABGPU_NSTAGE; k++) { p->stage_ms[k] = 0.0f; p->stage_n[k] = 0; }
     for (auto &r : p->ev_rec) {
         float t = 0.0f;
@@ -1153,6 +1185,13 @@ int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
         if (launches) launches[k] = p->stage_n[k];
     }
     return 0;
+}
+
+int dabgpu_pipe_sync(dabgpu_pipe *p) {
+    if (!p) return fail(DABGPU_E_ARG, "null pipe");
+    HIPCHK(hipStreamSynchronize(p->c->stream));
+    HIPCHK(hipStreamSynchronize(p->vs));
+    return kernel_errors(p->c);
 }
 
 int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, dabgpu_superframe *info) {
@@ -1179,7 +1218,9 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.info = info;
     J.tabs = c->dptab;
     HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, true));
-    HIPCHK(launch_dabplus(c->stream, J));
+    HIPCHK(launch_dabplus(p->vs, J));
+    // the next-but-one run waits for this too (it only reads the MSC output)
+    HIPCHK(hipEventRecord(p->ev_back[(p->run_idx - 1) & 1], p->vs));
     HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, false));
     p->last_msc = nullptr;                     // each run's CIFs enter the superframe layer once
     return 0;

@@ -93,6 +93,7 @@ def lib() -> C.CDLL:
             "dabgpu_msc_deconvolve": ([vp, vp, i64, vp, i32, vp, i64], i32),
             "dabgpu_rs_decode": ([vp, vp, i32, vp, vp], i32),
             "dabgpu_pipe_dabplus": ([vp, vp, C.c_int32, vp], i32),
+            "dabgpu_pipe_sync": ([vp], i32),
             "dabgpu_pipe_create": ([vp, vp, C.POINTER(vp)], i32), "dabgpu_pipe_destroy": ([vp], i32),
             "dabgpu_pipe_acquire": ([vp, vp, i64, vp, vp], i32),
             "dabgpu_pipe_run": ([vp, vp, i64, vp, vp, vp, vp, C.c_int32, vp], i32),
@@ -328,6 +329,7 @@ class Pipeline:
              "dabgpu_pipe_run")
         if not download:
             return valid
+        self.sync()
         fic = self.fic_d.download(np.uint8, (self.S, self.F, 4, 768))
         crc = self.crc_d.download(np.uint8, (self.S, self.F, 12))
         msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), self.msc_stride)) \
@@ -340,6 +342,7 @@ class Pipeline:
         _chk(lib().dabgpu_pipe_dabplus(self.h, self.sf_d.ptr, self.sf_stride, self.sfi_d.ptr), "dabgpu_pipe_dabplus")
         if not download:
             return None
+        self.sync()
         nd = len(self.dp)
         raw = self.sfi_d.download(np.uint8, self.S * 4 * self.F * nd * C.sizeof(Superframe))
         info = np.frombuffer(raw.tobytes(), dtype=SUPERFRAME_DTYPE).reshape(self.S, 4 * self.F, nd)
@@ -347,6 +350,11 @@ class Pipeline:
         return info, sf
 
     STAGES = ("prs_sync", "block0", "demod", "fic", "msc_acs", "msc_traceback", "dabplus")
+
+    def sync(self) -> None:
+        """wait for every stage of the last run (channel decoding runs on the
+        pipeline's own stream, overlapping the next run's front end)"""
+        _chk(lib().dabgpu_pipe_sync(self.h), "dabgpu_pipe_sync")
 
     def set_profiling(self, on: bool = True) -> None:
         _chk(lib().dabgpu_pipe_set_profiling(self.h, 1 if on else 0), "set_profiling")

@@ -239,6 +239,7 @@ bool ensembleDecoder::step() {
                                    valid.data());
     if (rc != DABGPU_OK && rc != DABGPU_E_STATE) chk(rc, "dabgpu_pipe_run");
     const bool ok = rc == DABGPU_OK;
+    chk(dabgpu_pipe_sync(pipe_), "dabgpu_pipe_sync");
     // frames committed per stream: FIC is delivered for those, MSC only on success
     std::vector<dabgpu_frame> fr((size_t)S * F);
     std::vector<int32_t> si((size_t)S * F);
@@ -269,6 +270,7 @@ bool ensembleDecoder::step() {
     if (ok && ndp_) {
         chk(dabgpu_pipe_dabplus(pipe_, (uint8_t *)sf_.get(), sf_stride_, (dabgpu_superframe *)sfi_.get()),
             "dabgpu_pipe_dabplus");
+        chk(dabgpu_pipe_sync(pipe_), "dabgpu_pipe_sync");
         if (sf_cb_) {
             std::vector<dabgpu_superframe> info((size_t)S * 4 * F * ndp_);
             std::vector<uint8_t> bytes(info.size() * sf_stride_);
