@@ -9,8 +9,12 @@
 
 namespace dab {
 
-constexpr int FFT_LDS_STRIDE = 66;       // float2 per transpose row (conflict-free b64 reads)
-constexpr int FFT_LDS_FLOAT2 = 32 * FFT_LDS_STRIDE;
+// The 32 x 64 transpose inside fft2048 runs one column parity at a time, so the
+// scratch holds 32 rows of 32 (+1 pad) float2: rows k1, column n2 >> 1.  Row
+// stride 33 float2 = 66 dwords puts the 32 rows a reader lane set touches in
+// distinct bank pairs (ds_read_b64: bank (a/4) mod 64).
+constexpr int FFT_LDS_STRIDE = 33;
+constexpr int FFT_LDS_FLOAT2 = 32 * FFT_LDS_STRIDE;     // 8,448 B per wave
 
 template <int I, int N, class F>
 __device__ __forceinline__ void sfor(F &&f) {
@@ -121,14 +125,66 @@ __device__ __forceinline__ void fft32(float2 (&v)[32]) {
 // tw : per-lane twiddle bases, loaded once per kernel by load_twiddles():
 //      A[a] = W2048^{n2*a} (a = 0..7), B[b] = W2048^{n2*8b} (b = 0..3), so that
 //      W2048^{n2*k1} = A[k1&7] * B[k1>>3] with one rounding.
-struct Twiddles { float2 A[8], B[4]; };
+struct Twiddles {
+    float2 A_[8], B_[4];
+    __device__ __forceinline__ float2 A(int a) const { return A_[a]; }
+    __device__ __forceinline__ float2 B(int b) const { return B_[b]; }
+};
+// the same bases read from a workgroup-shared LDS copy of the [12][64] table at
+// each use (k_demod: keeps 24 VGPRs free for the previous symbol's spectrum)
+struct TwiddlesLds {
+    const float2 *t;        // table + lane
+    __device__ __forceinline__ float2 A(int a) const { return t[a * 64]; }
+    __device__ __forceinline__ float2 B(int b) const { return t[(8 + b) * 64]; }
+};
 __device__ __forceinline__ void load_twiddles(Twiddles &t, const float2 *__restrict__ tab, int lane) {
 #pragma unroll
-    for (int a = 0; a < 8; a++) t.A[a] = tab[a * 64 + lane];                 // rows 0..7: n2*a
+    for (int a = 0; a < 8; a++) t.A_[a] = tab[a * 64 + lane];                // rows 0..7: n2*a
 #pragma unroll
-    for (int b = 0; b < 4; b++) t.B[b] = tab[(8 + b) * 64 + lane];           // rows 8..11: n2*8b
+    for (int b = 0; b < 4; b++) t.B_[b] = tab[(8 + b) * 64 + lane];          // rows 8..11: n2*8b
 }
-__device__ __forceinline__ void fft2048(float2 (&v)[32], float2 *lds, const Twiddles &tw, int lane) {
+// per-lane select by a constant lane mask: lanes in MASK take b, the others a.
+// As a v_cndmask on register values (a C select of two array elements may be
+// folded into one load through a selected pointer, which demotes the array to
+// scratch).
+template <uint64_t MASK>
+__device__ __forceinline__ float sel_lanes(float a, float b) {
+    float d;
+    asm("v_cndmask_b32_e64 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "s"(MASK));
+    return d;
+}
+
+// One column parity of the fft2048 transpose: lanes with r == PH write their 32
+// values (column k1 = lane>>1 of every row), then take back their own row k1.
+// Every lane issues the reads (no divergent branch: the register allocator would
+// otherwise keep old and new values live together); the other parity keeps its
+// registers through a select.
+template <int PH>
+__device__ __forceinline__ void fft_transpose_half(float2 (&v)[32], float2 *lds, int k1, int r) {
+    if (r == PH) {
+        sfor<0, 32>([&](auto kc) {
+            constexpr int q = decltype(kc)::value;
+            lds[q * FFT_LDS_STRIDE + k1] = v[brev5(q)];
+        });
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const float2 *row = lds + k1 * FFT_LDS_STRIDE;
+    constexpr uint64_t MINE = PH ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+    sfor<0, 32>([&](auto mc) {
+        constexpr int m = decltype(mc)::value;
+        const float2 t = row[m];
+        v[m] = make_float2(sel_lanes<MINE>(v[m].x, t.x), sel_lanes<MINE>(v[m].y, t.y));
+        if constexpr ((m & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+    });
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+template <class TW>
+__device__ __forceinline__ void fft2048(float2 (&v)[32], float2 *lds, const TW &tw, int lane) {
     fft32(v);
     sfor<0, 32>([&](auto kc) {
         constexpr int k1 = decltype(kc)::value;
@@ -136,22 +192,26 @@ __device__ __forceinline__ void fft2048(float2 (&v)[32], float2 *lds, const Twid
         float2 y = v[brev5(k1)];
         if constexpr (k1 != 0) {
             float2 w;
-            if constexpr (a == 0) w = tw.B[b];
-            else if constexpr (b == 0) w = tw.A[a];
+            if constexpr (a == 0) w = tw.B(b);
+            else if constexpr (b == 0) w = tw.A(a);
             else {
-                float2 ta = tw.A[a];
+                float2 ta = tw.A(a);
                 asm volatile("" : "+v"(ta.x), "+v"(ta.y));   // keep the product in the loop (no LICM spill)
-                w = cmul(ta, tw.B[b].x, tw.B[b].y);
+                const float2 tb = tw.B(b);
+                w = cmul(ta, tb.x, tb.y);
             }
             y = cmul(y, w.x, w.y);
         }
-        lds[k1 * FFT_LDS_STRIDE + lane] = y;
+        v[brev5(k1)] = y;
         if constexpr ((k1 & 7) == 7) __builtin_amdgcn_sched_barrier(0);
     });
+    // transpose: lane (k1 = lane>>1, r = lane&1) takes row k1, columns n2 = 2m + r.
+    // Lanes of parity r write all their 32 values (column n2>>1 of every row) and
+    // then read back their own row, so each phase frees exactly the registers it
+    // refills and the scratch holds half the matrix.
     const int k1 = lane >> 1, r = lane & 1;
-    const float2 *row = lds + k1 * FFT_LDS_STRIDE + r;
-#pragma unroll
-    for (int m = 0; m < 32; m++) v[m] = row[2 * m];
+    fft_transpose_half<0>(v, lds, k1, r);
+    fft_transpose_half<1>(v, lds, k1, r);
     fft32(v);
     const float sg = r ? -1.0f : 1.0f;
     sfor<0, 32>([&](auto ic) {

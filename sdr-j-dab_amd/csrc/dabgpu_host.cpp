@@ -102,16 +102,22 @@ struct HostTables {
         std::vector<int> carrier_of_bin(2048, -1);
         for (int c = 0; c < 1536; c++) { int k = perm[c]; carrier_of_bin[k < 0 ? k + 2048 : k] = c; }
         ref_l.resize(32 * 64);
-        cmap_l.resize(16 * 64);
+        cmap_l.assign((DEMOD_NPJ + 1) / 2 * 64, 0u);
         for (int lane = 0; lane < 64; lane++) {
             int k1 = lane >> 1, r = lane & 1;
-            for (int i = 0; i < 32; i++) {
-                int bin = k1 + 32 * brev5h(i) + 1024 * r;
-                ref_l[i * 64 + lane] = ref[bin];
-                uint32_t c = (uint32_t)(uint16_t)(int16_t)carrier_of_bin[bin];
-                if (i & 1) cmap_l[(i >> 1) * 64 + lane] |= c << 16;
-                else cmap_l[(i >> 1) * 64 + lane] = c;
+            for (int i = 0; i < 32; i++) ref_l[i * 64 + lane] = ref[k1 + 32 * brev5h(i) + 1024 * r];
+            // compact slot j <-> k2 = j + 8r: the bins of carriers +-1..768 (k_demod)
+            for (int j = 0; j < (DEMOD_NPJ + 1) / 2 * 2; j++) {
+                const int k2 = j + 8 * r;
+                const int c = k2 < 32 ? carrier_of_bin[k1 + 32 * k2 + 1024 * r] : -1;
+                const uint32_t w = (uint32_t)(uint16_t)(int16_t)c;
+                cmap_l[(j >> 1) * 64 + lane] |= (j & 1) ? w << 16 : w;
             }
+        }
+        for (int b = 0; b < 2048; b++) {      // every carrier bin lies in some lane's compact slots
+            const int k1 = b & 31, k2 = (b >> 5) & 31, r = b >> 10;
+            if (carrier_of_bin[b] >= 0 && (k2 - 8 * r < 0 || k2 - 8 * r >= DEMOD_NPJ)) abort();
+            (void)k1;
         }
         refarg.resize(18);
         for (int i = 0; i < 18; i++) {        // ofdm-decoder.cpp:71-74
