@@ -230,9 +230,10 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, co
 int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes_d, int32_t sf_stride, dabgpu_superframe *info_d);
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
 /* Wait until everything the pipeline enqueued is done.  The FIC/MSC/DAB+ outputs
- * of a run are written by the pipeline's own HIP stream (overlapping the next
- * run's OFDM front end): call this before reading them.  Also reports a kernel
- * that refused out-of-bounds work (DABGPU_E_BOUNDS). */
+ * of run r are written by back-end stream r & 1 (overlapping run r+1's OFDM front
+ * end and channel decoding): call this before reading them, and give run r+1
+ * output buffers other than run r's unless this was called in between.  Also
+ * reports a kernel that refused out-of-bounds work (DABGPU_E_BOUNDS). */
 int dabgpu_pipe_sync(dabgpu_pipe *p);
 /* per-stage kernel time of the last dabgpu_pipe_run (HIP events on the context
  * stream; enabling it adds one stream synchronisation at the end of each run) */

@@ -44,18 +44,17 @@ struct AcqResult {
 };
 
 // ---- Viterbi ------------------------------------------------------------
-constexpr int VCH = 48;                    // trellis steps per decision tile
+// decision words: per chunk of DEC_WORD_STEPS trellis steps and codeword row, 64
+// lanes x 32 bits (k_viterbi.hip: dec[(chunk * dec_ncw + row) * 64 + lane]); rows
+// padded to a whole traceback wave of 64
+constexpr int DEC_WORD_STEPS = 30;
+inline __host__ __device__ int64_t dec_rows(int n_cw) { return ((int64_t)n_cw + 63) / 64 * 64; }
+inline __host__ __device__ int64_t dec_bytes(int n_cw, int nbits) {
+    return (int64_t)((nbits + 6 + DEC_WORD_STEPS - 1) / DEC_WORD_STEPS) * dec_rows(n_cw) * 64 * 4;
+}
 
 // depuncturing profile: up to 4 (L_i, PI_i) segments + the 24-bit PI_X tail
 // (deconvolve.cpp:172-237, fic-handler.cpp:254-288)
-constexpr int TBC = 32;             // traceback chunk (steps per prefetch)
-// decision words per codeword for up to nbits decoded bits: whole ACS tiles
-// (VCH steps) and whole traceback chunks (TBC steps)
-inline __host__ __device__ int64_t dec_stride_for(int nbits) {
-    const int64_t t = (int64_t)(nbits + 6 + VCH - 1) / VCH * VCH;
-    return (t + TBC - 1) / TBC * TBC;
-}
-
 struct Profile {
     int32_t nbits;          // decoded bits N; trellis steps N+6
     int32_t nseg;           // 0 = no puncturing (mother code given directly)
@@ -90,8 +89,8 @@ struct VitJob {
     int32_t first_slot;             // ring slot of the batch's first frame
     const int32_t *sub_start;       // startAddr*64 per subchannel (up to 55232: int32)
     // outputs
-    uint64_t *dec;                  // decisions: one 64-bit word per trellis step
-    int64_t dec_stride;             // words per codeword row (dec_stride_for)
+    uint32_t *dec;                  // decision words (dec_bytes(n_cw, max nbits) bytes)
+    int64_t dec_ncw;                // rows of the decision buffer: >= dec_rows(n_cw)
     uint8_t *out;
     int64_t out_stride;             // bytes per codeword
     int32_t prbs;                   // xor energy-dispersal sequence

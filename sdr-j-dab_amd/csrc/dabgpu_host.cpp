@@ -469,12 +469,11 @@ int dabgpu_ofdm_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, in
 
 // ---- Viterbi operators -------------------------------------------------------
 static int run_viterbi(dabgpu_ctx *c, VitJob &J, int max_nbits) {
-    const int64_t ds = dec_stride_for(max_nbits);
     void *dec = nullptr;
-    int rc = scratch(c, SC_DEC, sizeof(uint64_t) * (size_t)J.n_cw * ds, &dec);
+    int rc = scratch(c, SC_DEC, (size_t)dec_bytes(J.n_cw, max_nbits), &dec);
     if (rc) return rc;
-    J.dec = (uint64_t *)dec;
-    J.dec_stride = ds;
+    J.dec = (uint32_t *)dec;
+    J.dec_ncw = dec_rows(J.n_cw);
     J.prbs_words = c->prbs;
     J.err = c->err;
     HIPCHK(launch_viterbi(c->stream, J));
@@ -635,7 +634,7 @@ struct dabgpu_pipe {
     int16_t *corr_d = nullptr;
     float *fc_d = nullptr, *fcpart_d = nullptr;
     int32_t *slots_d = nullptr;
-    uint64_t *dec_d = nullptr;
+    uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
     size_t dec_sz = 0;
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
@@ -649,11 +648,16 @@ struct dabgpu_pipe {
     const uint8_t *last_msc = nullptr; // MSC bits of the last successful run
     int32_t last_msc_stride = 0;
     int64_t last_cif0 = 0;
-    // channel decoding (FIC/MSC Viterbi, DAB+) runs on its own stream so run r's
-    // back end overlaps run r+1's front end; the ring holds 2F+4 frames per
-    // stream so run r+1's demod never overwrites a slot run r's MSC reads.
-    hipStream_t vs = nullptr;
-    hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr};
+    // channel decoding (FIC/MSC Viterbi, DAB+) of run r runs on back-end stream
+    // vs[r & 1], so run r's back end overlaps run r+1's front end AND run r+1's back
+    // end (whose first waves fill the SIMDs run r's last Viterbi waves leave idle).
+    // The ring holds 2F+4 frames per stream so run r+1's demod and MSC never touch a
+    // slot run r's MSC still reads; run r+2's front end waits for run r's back end.
+    // The caller gives consecutive runs different output buffers (or syncs).
+    hipStream_t vs[2] = {nullptr, nullptr};
+    int cur = 0;                                // back-end stream of the last run
+    hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr}, ev_dp = nullptr;
+    bool dp_rec = false;
     bool back_rec[2] = {false, false};
     int64_t run_idx = 0;
     Profile *ficprof_d = nullptr;
@@ -667,7 +671,7 @@ struct dabgpu_pipe {
 
 static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
     if (!p->profiling) return hipSuccess;
-    hipStream_t st = (stage >= DABGPU_STAGE_FIC) ? p->vs : p->c->stream;
+    hipStream_t st = (stage >= DABGPU_STAGE_FIC) ? p->vs[p->cur] : p->c->stream;
     if (start) {
         size_t need = 2 * (p->ev_rec.size() + 1);
         while (p->ev_pool.size() < need) {
@@ -743,12 +747,15 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->corr_d, sizeof(int16_t) * SF);
     A((void **)&p->fc_d, sizeof(float2) * SF);
     A((void **)&p->fcpart_d, sizeof(float2) * SF * kMaxChunks);
-    A((void **)&p->slots_d, sizeof(int32_t) * SF);
+    A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
     const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
-    p->dec_sz = sizeof(uint64_t) * ncw * (size_t)dec_stride_for(p->max_nbits);
-    A((void **)&p->dec_d, p->dec_sz);
+    p->dec_sz = (size_t)std::max(dec_bytes((int)ncw, p->max_nbits), dec_bytes(SF * 4, 768));
+    A((void **)&p->dec_d[0], p->dec_sz);
+    A((void **)&p->dec_d[1], p->dec_sz);
     A((void **)&p->ficprof_d, sizeof(Profile));
-    if (!rc && (hipStreamCreateWithFlags(&p->vs, hipStreamNonBlocking) != hipSuccess ||
+    if (!rc && (hipStreamCreateWithFlags(&p->vs[0], hipStreamNonBlocking) != hipSuccess ||
+                hipStreamCreateWithFlags(&p->vs[1], hipStreamNonBlocking) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_dp, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_front, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_back[0], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_back[1], hipEventDisableTiming) != hipSuccess))
@@ -801,14 +808,14 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
 int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     if (!p) return 0;
     (void)hipStreamSynchronize(p->c->stream);
-    if (p->vs) (void)hipStreamSynchronize(p->vs);
+    for (hipStream_t v : p->vs) if (v) (void)hipStreamSynchronize(v);
     for (auto e : p->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1]})
+    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1], p->ev_dp})
         if (e) (void)hipEventDestroy(e);
-    if (p->vs) (void)hipStreamDestroy(p->vs);
+    for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
-                    (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d,
+                    (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d})
         if (x) (void)hipFree(x);
     delete p;
@@ -1091,15 +1098,18 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     bool all = true;
     for (int s = 0; s < S; s++) if (done[s] != F) all = false;
     // channel decoding on the pipeline's stream, after this run's front end
+    p->cur = par;
+    hipStream_t bs = p->vs[par];
     HIPCHK(hipEventRecord(p->ev_front, c->stream));
-    HIPCHK(hipStreamWaitEvent(p->vs, p->ev_front, 0));
+    HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
     // FIC for every committed frame
     {
         std::vector<int32_t> slots((size_t)S * F);
         for (int s = 0; s < S; s++)
             for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = p->last_frames[(size_t)s * F + f].out_slot;
         if (fic_bits) {
-            HIPCHK(hipMemcpyAsync(p->slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, p->vs));
+            int32_t *slots_d = p->slots_d + (size_t)par * S * F;
+            HIPCHK(hipMemcpyAsync(slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, bs));
             void *pd = p->ficprof_d;
             VitJob J;
             memset(&J, 0, sizeof J);
@@ -1108,17 +1118,17 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             J.src = p->ring;
             J.src_len = (int64_t)S * p->R * FRAME_SOFT;
             J.err = c->err;
-            J.slots = p->slots_d;
+            J.slots = slots_d;
             J.prof = (const Profile *)pd;
             J.out = fic_bits;
             J.out_stride = 768;
             J.prbs = 1;
             J.prbs_words = c->prbs;
-            J.dec = p->dec_d;
-            J.dec_stride = dec_stride_for(768);
+            J.dec = p->dec_d[par];
+            J.dec_ncw = dec_rows(J.n_cw);
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-            HIPCHK(launch_viterbi(p->vs, J));
-            if (fic_crc) HIPCHK(launch_fic_post(p->vs, fic_bits, fic_crc, 12 * S * F));
+            HIPCHK(launch_viterbi(bs, J));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         }
     }
@@ -1143,16 +1153,16 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         J.out_stride = msc_stride;
         J.prbs = 1;
         J.prbs_words = c->prbs;
-        J.dec = p->dec_d;
-        J.dec_stride = dec_stride_for(p->max_nbits);
+        J.dec = p->dec_d[par];
+        J.dec_ncw = dec_rows(J.n_cw);
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs(p->vs, J));
+        HIPCHK(launch_acs(bs, J));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
-        HIPCHK(launch_traceback(p->vs, J));
+        HIPCHK(launch_traceback(bs, J));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
     }
-    HIPCHK(hipEventRecord(p->ev_back[par], p->vs));
+    HIPCHK(hipEventRecord(p->ev_back[par], bs));
     p->back_rec[par] = true;
     p->run_idx++;
     p->last_msc = (msc_bits && p->NSUB > 0 && all) ? msc_bits : nullptr;
@@ -1178,7 +1188,7 @@ int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
     if (!p || !ms) return fail(DABGPU_E_ARG, "bad args");
     // stages recorded since the last dabgpu_pipe_run started (incl. dabgpu_pipe_dabplus)
     HIPCHK(hipStreamSynchronize(p->c->stream));
-    HIPCHK(hipStreamSynchronize(p->vs));
+    for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
     for (int k = 0; k < DABGPU_NSTAGE; k++) { p->stage_ms[k] = 0.0f; p->stage_n[k] = 0; }
     for (auto &r : p->ev_rec) {
         float t = 0.0f;
@@ -1196,7 +1206,7 @@ int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
 int dabgpu_pipe_sync(dabgpu_pipe *p) {
     if (!p) return fail(DABGPU_E_ARG, "null pipe");
     HIPCHK(hipStreamSynchronize(p->c->stream));
-    HIPCHK(hipStreamSynchronize(p->vs));
+    for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
     return kernel_errors(p->c);
 }
 
@@ -1223,11 +1233,17 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.sf_stride = sf_stride;
     J.info = info;
     J.tabs = c->dptab;
+    // on the last run's back-end stream (after its MSC), after the previous
+    // superframe pass (the 5-CIF rings carry state from run to run)
+    hipStream_t bs = p->vs[p->cur];
+    if (p->dp_rec) HIPCHK(hipStreamWaitEvent(bs, p->ev_dp, 0));
     HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, true));
-    HIPCHK(launch_dabplus(p->vs, J));
-    // the next-but-one run waits for this too (it only reads the MSC output)
-    HIPCHK(hipEventRecord(p->ev_back[(p->run_idx - 1) & 1], p->vs));
+    HIPCHK(launch_dabplus(bs, J));
     HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, false));
+    HIPCHK(hipEventRecord(p->ev_dp, bs));
+    p->dp_rec = true;
+    // the next-but-one run waits for this too (it only reads the MSC output)
+    HIPCHK(hipEventRecord(p->ev_back[p->cur], bs));
     p->last_msc = nullptr;                     // each run's CIFs enter the superframe layer once
     return 0;
 }

@@ -6,28 +6,43 @@
 //   strict ">" picks the upper predecessor; full chainback from state 0.
 //
 // gfx950 design
-//   k_acs       one wave64 per codeword, one trellis state per lane.  States
-//               are relabelled every step (lane L holds state rotl6(L, t mod 6))
-//               so each ACS butterfly is a single lane-pair exchange at xor
-//               distance 32,16,8,4,2,1 (permlane32/16_swap, DPP) instead of a
-//               64-way shuffle.  Branch metrics for 48 steps are built in LDS by
-//               48 lanes at once (depuncturing + 16-CIF time de-interleave fused
-//               into that gather).  The 64 decisions of a step come straight
-//               from two v_cmp masks and land in HBM as 48-step tiles.
-//   k_traceback one LANE per codeword: 64 chainbacks per wave in lock-step,
-//               reading the decision tiles; bits leave through 16-B stores
-//               with the energy-dispersal PRBS xor-ed in.
+//   k_acs       one wave64 per PAIR of codewords, one trellis state per lane, the two
+//               codewords' path metrics packed in the 16-bit halves of one VGPR
+//               (v_pk_add_u16 / v_pk_min_u16 do both).  Exactness of 16 bits: metric
+//               spread across states is <= 6 * 1020 (every state is reachable from the
+//               best one in 6 steps, branch metrics are in [0, 1020]), so subtracting a
+//               common offset every 48 steps keeps every metric in [0, 61326] and every
+//               comparison equal to the reference's uint32 one.
+//               States are relabelled every step (lane L holds state rotl6(L, t mod 6)),
+//               so a butterfly pairs lanes at xor distance 32,16,8,4,2,1.  Each lane
+//               forms its two candidates as (metric of the LOWER lane of its pair) +
+//               row A and (metric of the UPPER lane) + row B, the rows chosen per lane
+//               so that the decision is "cand0 > cand1" in every lane: one compare per
+//               codeword per step.  The broadcasts are DPP (quad_perm, row_shr/shl with
+//               bank masks) or one permlane16/32_swap.  Each lane shifts its decision
+//               bits into a 32-bit word per codeword (v_addc with the compare mask as
+//               carry-in) and stores it every 32 steps: decisions never leave the VGPRs
+//               as scalar masks.  Branch metrics for 96 steps are built in LDS by the
+//               lanes at once (depuncturing + 16-CIF time de-interleave fused into that
+//               gather), both codewords packed per word.
+//   k_traceback one LANE per codeword, 64 chainbacks per wave in lock-step.  Decision
+//               words of a 32-step chunk for the wave's 64 codewords are staged in LDS
+//               (16 KB, double-buffered against the next chunk's loads); each step reads
+//               the word of the lane that held the traced state.  Bits leave through
+//               4-B stores with the energy-dispersal PRBS xor-ed in.
+//
+// Decision layout: dec[(chunk * dec_ncw + row) * 64 + lane] (uint32), bit (31 - k) =
+// decision of `lane` at trellis step 32*chunk + k.
 #include "dab_device.h"
 #include "dab_kernels.h"
 
 namespace dab {
 
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u16x2 as_pk(uint32_t v) { return __builtin_bit_cast(u16x2, v); }
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) { return __builtin_bit_cast(uint32_t, v); }
+
 __device__ __forceinline__ int rotl6(int x, int r) { return ((x << r) | (x >> (6 - r))) & 63; }
-__device__ __forceinline__ int delay16(int i) {         // dab-concurrent.cpp:42-43
-    int b = i & 15;
-    int rv = ((b & 1) << 3) | ((b & 2) << 1) | ((b & 4) >> 1) | ((b & 8) >> 3);
-    return 15 - rv;
-}
 
 // XCD-aware block order (cdna_hip_programming.md T1): blocks b with equal b % 8
 // share an XCD's L2; give each such group a contiguous range of codewords so the
@@ -35,6 +50,12 @@ __device__ __forceinline__ int delay16(int i) {         // dab-concurrent.cpp:42
 __device__ __forceinline__ int xcd_order(int b, int n) {
     const int q = n >> 3, r = n & 7, x = b & 7;
     return (x < r ? x * (q + 1) : r * (q + 1) + (x - r) * q) + (b >> 3);
+}
+
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
 // Per-codeword source, resolved once per wave.
@@ -46,13 +67,14 @@ struct Src {
 };
 
 // SRC_MSC logical order (stream, subchannel, CIF) -- consecutive CIFs of one
-// subchannel share 15 of their 16 source rows; output rows stay
+// subchannel share 15 of their 16 source rows and their profile; output rows stay
 // ((stream * ncif) + cif) * nsub + sub.
 template <int KIND>
 __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *rowoff, int lane) {
     Src c;
     c.prof = 0;
-    c.valid = true;
+    c.valid = logical < J.n_cw;
+    if (!c.valid) logical = 0;
     c.row = logical;
     if constexpr (KIND == SRC_MOTHER) {
         c.base = J.src + (int64_t)logical * J.src_stride;
@@ -69,7 +91,7 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
         c.row = (stream * J.ncif + cl) * J.nsub + sub;
         c.prof = sub;
         const int64_t cif = J.cif0 + cl;
-        c.valid = cif >= 16;                           // dab-concurrent.cpp:172-175 warm-up
+        c.valid = c.valid && cif >= 16;                // dab-concurrent.cpp:172-175 warm-up
         c.base = J.src + (int64_t)stream * J.ring * FRAME_SOFT;
         if (lane < 16) {
             // element idx of CIF n comes from CIF n - d[idx & 15] (dab-concurrent.cpp:42-43,162-169)
@@ -88,28 +110,23 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
             }
             rowoff[lane] = ro;
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        wave_sync();
     }
-    if (J.valid && !J.valid[c.row]) c.valid = false;
+    if (c.valid && J.valid && !J.valid[c.row]) c.valid = false;
     if constexpr (KIND != SRC_MSC) {
-        const Profile &P = J.prof[c.prof];
-        const int64_t need = P.nseg ? P.frag : 4 * (int64_t)(P.nbits + 6);
-        const int64_t o = c.base - J.src;
-        if (c.valid && (o < 0 || o + need > J.src_len)) {   // never read outside the buffer
-            if (lane == 0) atomicOr(J.err, KERR_VITERBI);
-            c.valid = false;
+        if (c.valid) {
+            const Profile &P = J.prof[c.prof];
+            const int64_t need = P.nseg ? P.frag : 4 * (int64_t)(P.nbits + 6);
+            const int64_t o = c.base - J.src;
+            if (o < 0 || o + need > J.src_len) {      // never read outside the buffer
+                if (lane == 0) atomicOr(J.err, KERR_VITERBI);
+                c.valid = false;
+            }
         }
     }
     return c;
 }
 
-// Element offsets (from c.base) of the 4 mother-code soft values of trellis step t
-// (positions 4t..4t+3) with the depuncturing of deconvolve.cpp:172-237 /
-// fic-handler.cpp:241-270.  keep bit e = 0 marks an erasure ("a real do not know",
-// fic-handler.cpp:259, or the zero tail of deconvolve.cpp:182); its offset is a
-// safe in-bounds dummy so the 4 loads can be issued unconditionally.
 // a Profile as wave-uniform registers: only constant indices below, so nothing
 // spills to scratch and nothing goes through the vector memory queue
 struct ProfR {
@@ -140,220 +157,293 @@ __device__ __forceinline__ ProfR prof_regs(const Profile *p) {
     return r;
 }
 
-template <int KIND>
-__device__ __forceinline__ uint32_t addr4(const int32_t *rowoff, const ProfR *__restrict__ pp, int t, int (&o)[4]) {
-    const ProfR &P = *pp;
+// Input indices (relative to the codeword's punctured fragment) of the 4 mother-code
+// soft values of trellis step t (positions 4t..4t+3) with the depuncturing of
+// deconvolve.cpp:172-237 / fic-handler.cpp:241-270.  keep bit e = 0 marks an erasure
+// ("a real do not know", fic-handler.cpp:259, or the zero tail of deconvolve.cpp:182).
+__device__ __forceinline__ uint32_t idx4(const ProfR &P, int t, int (&idx)[4]) {
     const int p = 4 * t;
-    uint32_t keep = 0;
-    int idx[4] = {0, 0, 0, 0};
     if (P.nseg == 0) {
 #pragma unroll
         for (int e = 0; e < 4; e++) idx[e] = p + e;
-        keep = 0xF;
-    } else {
-        const int blk = p >> 7;
-        uint32_t m = 0;
-        int base = 0, b = 0;
-        if (blk < P.last_end) {
-            // segment of this block: selects over the (wave-uniform) profile words,
-            // no per-lane indexing
-            int bs = 0, ib = P.in_base[0];
-            m = P.mask[0];
-#pragma unroll
-            for (int k = 1; k < 4; k++) {
-                if (k < P.nseg && blk >= P.blk_end[k - 1]) { bs = P.blk_end[k - 1]; ib = P.in_base[k]; m = P.mask[k]; }
-            }
-            const int bis = blk - bs;
-            const int n1 = __popc(m);
-            const int oo = p & 127;
-            b = oo & 31;
-            base = ib + bis * 4 * n1 + (oo >> 5) * n1;
-        } else {
-            b = p - 128 * P.last_end;
-            m = b < 24 ? P.tail_mask : 0u;
-            base = P.tail_base;
-            if (b >= 24) b = 0;
-        }
-        const uint32_t k4 = (m >> b) & 0xFu;
-        int i = base + __popc(m & ((1u << b) - 1u));
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            idx[e] = i;
-            i += (k4 >> e) & 1;
-        }
-        keep = k4;
+        return 0xF;
     }
+    const int blk = p >> 7;
+    uint32_t m = 0;
+    int base = 0, b = 0;
+    if (blk < P.last_end) {
+        // segment of this block: selects over the (wave-uniform) profile words
+        int bs = 0, ib = P.in_base[0];
+        m = P.mask[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++) {
+            if (k < P.nseg && blk >= P.blk_end[k - 1]) { bs = P.blk_end[k - 1]; ib = P.in_base[k]; m = P.mask[k]; }
+        }
+        const int bis = blk - bs;
+        const int n1 = __popc(m);
+        const int oo = p & 127;
+        b = oo & 31;
+        base = ib + bis * 4 * n1 + (oo >> 5) * n1;
+    } else {
+        b = p - 128 * P.last_end;
+        m = b < 24 ? P.tail_mask : 0u;
+        base = P.tail_base;
+        if (b >= 24) b = 0;
+    }
+    const uint32_t k4 = (m >> b) & 0xFu;
+    int i = base + __popc(m & ((1u << b) - 1u));
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        idx[e] = i;
+        i += (k4 >> e) & 1;
+    }
+    return k4;
+}
+
+// the 4 soft values of one step of one codeword into half H of s[] (erasures and
+// steps past the codeword's end read as 0)
+template <int KIND, int H>
+__device__ __forceinline__ void load4(const Src &c, const int32_t *rowoff, const int (&idx)[4], uint32_t keep,
+                                      u16x2 (&s)[4]) {
 #pragma unroll
     for (int e = 0; e < 4; e++) {
         int off = idx[e];
+        bool k = (keep >> e) & 1u;
         if constexpr (KIND == SRC_MSC) {
             const int ro = rowoff[idx[e] & 15];
-            if (ro < 0) keep &= ~(1u << e);          // delay line still empty: zero
+            k = k && ro >= 0;                         // delay line still empty: zero
             off = ro + idx[e];
         }
-        o[e] = ((keep >> e) & 1u) ? off : 0;
+        const unsigned short v = (unsigned short)c.base[k ? off : 0];
+        s[e][H] = k ? v : (unsigned short)0;
     }
-    return keep;
 }
 
 __device__ __forceinline__ int parity(int v) { return __popc(v) & 1; }
 
-template <int RHO>
-struct LaneMask {            // lanes whose bit (5-RHO) is set = lanes holding an upper (msb=1) state
-    static constexpr uint64_t v = RHO == 0 ? 0xFFFFFFFF00000000ull : RHO == 1 ? 0xFFFF0000FFFF0000ull
-                                : RHO == 2 ? 0xFF00FF00FF00FF00ull : RHO == 3 ? 0xF0F0F0F0F0F0F0F0ull
-                                : RHO == 4 ? 0xCCCCCCCCCCCCCCCCull : 0xAAAAAAAAAAAAAAAAull;
-};
+// LDS branch-metric table for a tile of VT steps: 8 rows q (the (b0,b1,b2) output
+// pattern); step j of row q holds the pair {bm[q], bm[q^7]} as two packed words
+// (codeword A in the low, B in the high 16 bits).  The row stride puts the 8 rows one
+// ds_read_b64 touches in 8 distinct bank pairs.
+constexpr int WS = DEC_WORD_STEPS;         // 30 decisions per word: a multiple of 6, so
+                                           // every word starts at relabelling phase 0
+constexpr int VT = 2 * WS;                 // steps per branch-metric tile (lanes 0..59 build one each)
+constexpr int BRS = 2 * VT + 2;            // 122: rows 0..7 start at banks 0,58,52,46,40,34,28,22
+static_assert(WS % 6 == 0 && (BRS & 3) == 2, "bank-pair stride");
+constexpr int RENORM = WS;                 // steps between metric renormalisations (see header)
+constexpr uint32_t SPREAD = 6 * 1020;
 
-// Row stride of the branch-metric table: odd, so the 8 rows that one ACS step
-// reads (8 distinct words, broadcast to 64 lanes) sit in 8 different LDS banks.
-constexpr int BMS = VCH + 1;
+// branch metrics of one step for the 8 (b0,b1,b2) output patterns, both codewords
+// (viterbi.cpp:159-164: metric = sum_j sym_j ^ B_j with b3 = b0; y ^ 255 = 255 - y).
+// Every partial sum stays inside its 16-bit half, so plain 32-bit adds work on pairs.
+__device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4]) {
+    typedef short i16x2 __attribute__((ext_vector_type(2)));
+    uint32_t y[4];
+#pragma unroll
+    for (int e = 0; e < 4; e++) {                 // clamp(s + 127, 0, 255) per half
+        const i16x2 v = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2, s[e]),
+                                                                            (i16x2){-127, -127}), (i16x2){128, 128});
+        y[e] = as_u32(__builtin_bit_cast(u16x2, v) + (u16x2){127, 127});
+    }
+    const uint32_t a0 = y[0] + y[3], a1 = 0x01FE01FEu - a0;
+    const uint32_t b0 = y[1] + y[2], b1 = 0x00FF00FFu - y[1] + y[2], b2 = 0x00FF00FFu + y[1] - y[2],
+                   b3 = 0x01FE01FEu - b0;
+    const uint32_t w[4] = {a0 + b0, a1 + b0, a0 + b1, a1 + b1};           // q = 0..3
+    const uint32_t wc[4] = {a1 + b3, a0 + b3, a1 + b2, a0 + b2};          // q ^ 7 = 7..4
+    // q = 0..3: {bm[q], bm[7-q]};  q = 4..7: {bm[q], bm[7-q]} = {wc[7-q], w[7-q]}
+#pragma unroll
+    for (int q = 0; q < 4; q++) *(uint2 *)&bm[q * BRS + 2 * j] = make_uint2(w[q], wc[q]);
+#pragma unroll
+    for (int q = 4; q < 8; q++) *(uint2 *)&bm[q * BRS + 2 * j] = make_uint2(wc[7 - q], w[7 - q]);
+}
 
-// branch metrics of one step for the 8 (b0,b1,b2) output patterns
-// (viterbi.cpp:159-164: metric = sum_j sym_j ^ B_j with b3 = b0)
-__device__ __forceinline__ void put_bm(uint32_t *bm, const int16_t (&s)[4], uint32_t keep, int lane) {
-    if (lane < VCH) {
-        int y[4];
-#pragma unroll
-        for (int e = 0; e < 4; e++) y[e] = min(max(((keep >> e) & 1u ? (int)s[e] : 0) + 127, 0), 255);
-        // y ^ 255 = 255 - y on [0, 255]: 4 partial sums instead of 8 x 4 xors
-        const int a[2] = {y[0] + y[3], 510 - (y[0] + y[3])};
-        const int bc[4] = {y[1] + y[2], 255 - y[1] + y[2], 255 + y[1] - y[2], 510 - (y[1] + y[2])};
-#pragma unroll
-        for (int q = 0; q < 8; q++) bm[q * BMS + lane] = (uint32_t)(a[q & 1] + bc[q >> 1]);
+// (P, Q) = metric of the lower / upper lane of this lane's butterfly pair (xor M)
+template <int M>
+__device__ __forceinline__ void bcast(uint32_t x, uint32_t &P, uint32_t &Q) {
+    if constexpr (M == 1) {
+        P = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xF, 0xF, false);        // quad_perm [0,0,2,2]
+        Q = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xF5, 0xF, 0xF, false);        // quad_perm [1,1,3,3]
+    } else if constexpr (M == 2) {
+        P = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x44, 0xF, 0xF, false);        // quad_perm [0,1,0,1]
+        Q = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xEE, 0xF, 0xF, false);        // quad_perm [2,3,2,3]
+    } else if constexpr (M == 4) {
+        // upper lanes (banks 1,3 of each row) take lane-4; lower lanes (banks 0,2) lane+4
+        Q = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x104, 0xF, 0x5, false);  // row_shl:4
+        P = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xF, 0xA, false);  // row_shr:4
+    } else if constexpr (M == 8) {
+        Q = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x108, 0xF, 0x3, false);  // row_shl:8
+        P = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x118, 0xF, 0xC, false);  // row_shr:8
+    } else if constexpr (M == 16) {
+        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);   // odd rows <-> even rows
+        P = r[0];
+        Q = r[1];
+    } else {
+        static_assert(M == 32, "xor distance");
+        auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
+        P = r[0];
+        Q = r[1];
     }
 }
 
-// ACS over one tile of nst (<= VCH) trellis steps.  1020 - bm[q] = bm[q ^ 7].
-// Returns the tile's decision word of step `lane` (lanes < nst).
-template <bool FULL>
-__device__ __forceinline__ uint64_t acs_tile(const uint32_t *bm, const uint32_t (&off)[6], const uint32_t (&offc)[6],
-                                             uint32_t &x, int lane, int nst) {
-    uint32_t dlo = 0, dhi = 0;
-    sfor<0, VCH / 6>([&](auto gc) {
-        sfor<0, 6>([&](auto rc) {
-            constexpr int rho = decltype(rc)::value;
-            constexpr int j = decltype(gc)::value * 6 + rho;
-            if (FULL || j < nst) {
-                const uint32_t a = x + bm[off[rho] + j];
-                const uint32_t b = xchg<(32 >> rho)>(x, lane) + bm[offc[rho] + j];
-                const uint64_t G = __ballot(a > b), Lt = __ballot(b > a);
-                constexpr uint64_t M = LaneMask<rho>::v;
-                const uint64_t D = (G & ~M) | (Lt & M);
-                dlo = (uint32_t)llvm_amdgcn_writelane((int)(uint32_t)D, j, (int)dlo);
-                dhi = (uint32_t)llvm_amdgcn_writelane((int)(uint32_t)(D >> 32), j, (int)dhi);
-                x = min(a, b);
-            }
-        });
-    });
-    return ((uint64_t)dhi << 32) | dlo;
+// acc = 2*acc + (lane's bit of mask): the decision enters as the carry-in
+__device__ __forceinline__ uint32_t shift_in(uint32_t acc, uint64_t mask) {
+    uint32_t r;
+    uint64_t co;
+    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(acc), "s"(mask));
+    return r;
 }
 
-template <int KIND>
-__global__ __launch_bounds__(64) void k_acs(VitJob J) {
-    __shared__ uint32_t bm[8 * BMS];
-    __shared__ int32_t rowoff[16];
+// subtract a common offset from all states of each codeword (see header)
+__device__ __forceinline__ uint32_t renorm(uint32_t x) {
+    const uint32_t x0 = __builtin_amdgcn_readfirstlane(x);
+    const uint32_t lo = x0 & 0xFFFFu, hi = x0 >> 16;
+    const uint32_t c = (lo > SPREAD ? lo - SPREAD : 0u) | ((hi > SPREAD ? hi - SPREAD : 0u) << 16);
+    return as_u32(as_pk(x) - as_pk(c));
+}
+
+// ACS over one decision word (WS trellis steps, or nst < WS for the last one) for NP
+// codeword pairs (independent chains, interleaved step by step).  bm: this word's
+// half of the tile table.  The words are stored at chunk `ch`; rb[k]: word offset of
+// codeword k's chunk 0 in dec (wave-uniform; < 0: not stored).  One copy of this code
+// serves every word (small hot loop: the instruction cache holds it).
+template <int NP, bool FULL>
+__device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP],
+                                         uint32_t (&acc)[2 * NP], int nst, uint32_t *dec,
+                                         const int64_t (&rb)[2 * NP], int64_t o, int lane) {
+    sfor<0, WS>([&](auto jc) {
+        constexpr int j = decltype(jc)::value;
+        constexpr int rho = j % 6;
+        if (FULL || j < nst) {
+            sfor<0, NP>([&](auto pc) {
+                constexpr int p = decltype(pc)::value;
+                uint32_t P, Q;
+                bcast<(32 >> rho)>(x[p], P, Q);
+                const uint2 t = *(const uint2 *)(bm + p * 8 * BRS + row[rho] + 2 * j);
+                const u16x2 A = as_pk(P) + as_pk(t.x), B = as_pk(Q) + as_pk(t.y);
+                acc[2 * p] = shift_in(acc[2 * p], __builtin_amdgcn_ballot_w64(A.x > B.x));
+                acc[2 * p + 1] = shift_in(acc[2 * p + 1], __builtin_amdgcn_ballot_w64(A.y > B.y));
+                x[p] = as_u32(__builtin_elementwise_min(A, B));
+            });
+        }
+    });
+    const int sh = FULL ? 0 : WS - nst;                  // step k of the word at bit WS-1-k
+#pragma unroll
+    for (int k = 0; k < 2 * NP; k++)
+        if (rb[k] >= 0) (dec + rb[k] + o)[lane] = acc[k] << sh;
+#pragma unroll
+    for (int p = 0; p < NP; p++) x[p] = renorm(x[p]);
+}
+
+// NP pairs of codewords per wave: codewords 2*NP*w .. 2*NP*w + 2*NP - 1 (logical order)
+template <int KIND, int NP>
+__global__ __launch_bounds__(64, 8) void k_acs(VitJob J) {
+    __shared__ uint32_t bm[NP * 8 * BRS];
+    __shared__ int32_t rowoff[2 * NP][16];
     const int lane = threadIdx.x;
-    const Src c = src_of<KIND>(J, xcd_order(blockIdx.x, gridDim.x), rowoff, lane);
-    if (!c.valid) return;
-    // the profile is wave-uniform: scalar loads, kept out of the vector memory queue
-    const ProfR prof = prof_regs(J.prof + c.prof);       // in registers for the whole codeword
-    const ProfR *pp = &prof;
-    const int steps = prof.nbits + 6;
-    uint32_t off[6], offc[6];
+    const int w = xcd_order(blockIdx.x, gridDim.x);
+    Src c[2 * NP];
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < 2 * NP; k++) {
+        c[k] = src_of<KIND>(J, 2 * NP * w + k, rowoff[k], lane);
+        any = any || c[k].valid;
+    }
+    if (!any) return;
+    // profiles are wave-uniform: scalar loads, kept out of the vector memory queue
+    const ProfR p0 = prof_regs(J.prof + c[0].prof);
+    bool same = true;
+    int stp[2 * NP], steps = 0;
+#pragma unroll
+    for (int k = 0; k < 2 * NP; k++) {
+        same = same && c[k].prof == c[0].prof;
+        stp[k] = c[k].valid ? __builtin_amdgcn_readfirstlane(J.prof[c[k].prof].nbits) + 6 : 0;
+        steps = max(steps, stp[k]);
+    }
+    // per-lane LDS row of each relabelling phase (see header): q = output pattern of
+    // butterfly i = rotl6(lane, r) & 31; upper lanes of a pair swap the two rows
+    uint32_t row[6];
 #pragma unroll
     for (int r = 0; r < 6; r++) {
-        const int i = rotl6(lane, r) & 31;               // butterfly of the state this lane holds
+        const int i = rotl6(lane, r) & 31;
         const int q = parity((2 * i) & 0155) | (parity((2 * i) & 0117) << 1) | (parity((2 * i) & 0123) << 2);
-        off[r] = (uint32_t)(q * BMS);
-        offc[r] = (uint32_t)((q ^ 7) * BMS);
+        const bool upper = (lane >> (5 - r)) & 1;
+        row[r] = (uint32_t)((upper ? q ^ 7 : q) * BRS);
     }
-    uint32_t x = lane == 0 ? 0u : 63u;                   // viterbi.cpp:360-371
-    uint64_t *dec = J.dec + (int64_t)c.row * J.dec_stride;
-    // inputs of the next tile are loaded while the current one runs its ACS
-    int16_t s[4];
-    uint32_t keep;
-    auto fetch = [&](int t) {
-        int o[4];
-        keep = 0;
-        if (lane < VCH && t < steps) keep = addr4<KIND>(rowoff, pp, t, o);
-        else o[0] = o[1] = o[2] = o[3] = 0;
+    uint32_t x[NP], acc[2 * NP];
+    int64_t rb[2 * NP];
 #pragma unroll
-        for (int e = 0; e < 4; e++) s[e] = c.base[o[e]];
-    };
-    // A tile's decisions are stored one tile late, just BEFORE the next prefetch:
-    // vmcnt counts stores too, so the wait for the prefetched inputs then never
-    // has to wait for a store issued after them.
-    fetch(lane);
-    uint64_t dprev = 0;
-    int tprev = -1;
-    int t0 = 0;
-    for (; t0 + VCH <= steps; t0 += VCH) {
-        put_bm(bm, s, keep, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        if (tprev >= 0 && lane < VCH) dec[tprev + lane] = dprev;
-        fetch(t0 + VCH + lane);
-        dprev = acs_tile<true>(bm, off, offc, x, lane, VCH);
-        tprev = t0;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int p = 0; p < NP; p++) x[p] = lane == 0 ? 0u : 0x003F003Fu;   // viterbi.cpp:360-371
+#pragma unroll
+    for (int k = 0; k < 2 * NP; k++) {
+        acc[k] = 0;
+        rb[k] = c[k].valid ? (int64_t)c[k].row * 64 : -1;
     }
-    if (tprev >= 0 && lane < VCH) dec[tprev + lane] = dprev;
-    if (t0 < steps) {
-        put_bm(bm, s, keep, lane);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        const uint64_t d = acs_tile<false>(bm, off, offc, x, lane, steps - t0);
-        if (lane < steps - t0) dec[t0 + lane] = d;
+    const int64_t cstride = J.dec_ncw * 64;
+    // inputs of the next tile are loaded while the current one runs its ACS;
+    // lane < VT handles step t0 + lane
+    u16x2 s[NP][4];                                      // packed {A, B} soft values, per pair
+    auto fetch = [&](int t) {
+        int i0[4];
+        uint32_t k0 = 0;
+        if (t < stp[0] || (same && t < steps)) k0 = idx4(p0, t, i0);
+        else i0[0] = i0[1] = i0[2] = i0[3] = 0;
+        sfor<0, 2 * NP>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            int ik[4];
+            uint32_t kk;
+            if (same) {
+                kk = t < stp[k] ? k0 : 0u;
+#pragma unroll
+                for (int e = 0; e < 4; e++) ik[e] = i0[e];
+            } else {
+                kk = 0;
+                ik[0] = ik[1] = ik[2] = ik[3] = 0;
+                if (t < stp[k]) kk = idx4(prof_regs(J.prof + c[k].prof), t, ik);
+            }
+            load4<KIND, k & 1>(c[k], rowoff[k], ik, kk, s[k >> 1]);
+        });
+    };
+    auto put = [&]() {
+#pragma unroll
+        for (int p = 0; p < NP; p++) put_bm(bm + p * 8 * BRS, lane, s[p]);
+    };
+    const bool mine = lane < VT;                         // lanes that build a step of the table
+    fetch(mine ? lane : steps);
+    for (int t0 = 0; t0 < steps; t0 += VT) {
+        if (mine) put();
+        wave_sync();
+        fetch(mine ? t0 + VT + lane : steps);
+        for (int u = 0; u < 2; u++) {
+            const int tw = t0 + u * WS;
+            if (tw >= steps) break;
+            const int64_t o = (int64_t)(tw / WS) * cstride;
+            if (tw + WS <= steps) acs_word<NP, true>(bm + 2 * WS * u, row, x, acc, WS, J.dec, rb, o, lane);
+            else acs_word<NP, false>(bm + 2 * WS * u, row, x, acc, steps - tw, J.dec, rb, o, lane);
+        }
+        wave_sync();
     }
 }
 
-// Chainback (viterbi.cpp:333-357) from state 0, one lane per codeword.  The
-// decision words of a lane are contiguous; TBC-step chunks stream through a
-// 3-deep register ring (two chunks in flight while one is walked), so the
-// dependent bit walk does not wait on memory.
-template <bool CHECK>
-__device__ __forceinline__ void tb_chunk(const uint4 (&c)[TBC / 2], int ch, int steps, int N, int &lr, int &rho,
-                                         bool act, uint8_t *out, const VitJob &J) {
-    uint32_t w = 0;
+// Chainback (viterbi.cpp:333-357) from state 0, one lane per codeword.  The 64
+// codewords' decision words of chunk c (16 KB, contiguous) are staged in LDS; lane l
+// reads word [l][lr] where lr is the lane that held its traced state.  A chunk is
+// one word of WS steps starting at relabelling phase 0, so the bit positions and the
+// phase of every step are compile-time constants.
+constexpr int TB_WORDS = 64 * 64;          // one chunk of a wave's 64 codewords
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 copies as a memcpy -> scratch)
+__device__ __forceinline__ void tb_load(u32x4 (&r)[16], const uint32_t *blk, int lane) {
+    const u32x4 *q = (const u32x4 *)blk;
 #pragma unroll
-    for (int k = TBC - 1; k >= 0; k--) {
-        const int t = ch * TBC + k;
-        const uint32_t Dlo = (k & 1) ? c[k >> 1].z : c[k >> 1].x;
-        const uint32_t Dhi = (k & 1) ? c[k >> 1].w : c[k >> 1].y;
-        const int p = 5 - rho;
-        const int u = (lr >> p) & 1;                                   // decoded bit of step t
-        const uint32_t Dw = (lr & 32) ? Dhi : Dlo;
-        const int d = (int)((Dw >> (lr & 31)) & 1u);                   // predecessor's msb
-        const int nl = (lr & ~(1 << p)) | (d << p);
-        if (!CHECK || t < steps) {
-            lr = nl;
-            w |= (uint32_t)u << k;
-        }
-        rho = rho == 0 ? 5 : rho - 1;
-    }
-    const int t0 = ch * TBC;
-    if (act && t0 < N) {
-        if (J.prbs) w ^= J.prbs_words[t0 >> 5];
-        if (t0 + 32 <= N) {
+    for (int i = 0; i < 16; i++) r[i] = q[i * 64 + lane];
+}
+__device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[16], int lane) {
 #pragma unroll
-            for (int e = 0; e < 8; e++) {
-                const uint32_t nib = (w >> (4 * e)) & 0xFu;
-                *(uint32_t *)(out + t0 + 4 * e) = (nib * 0x00204081u) & 0x01010101u;
-            }
-        } else {
-            for (int i = 0; t0 + i < N; i++) out[t0 + i] = (uint8_t)((w >> i) & 1u);
-        }
-    }
+    for (int i = 0; i < 16; i++) ((u32x4 *)lds)[i * 64 + lane] = r[i];
 }
 
 template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
-    static_assert(TBC == 32, "one 32-bit output word per chunk");
+    __shared__ uint32_t stage[2][TB_WORDS];
     const int lane = threadIdx.x, cw = blockIdx.x * 64 + lane;
     bool act = cw < J.n_cw;
     int N = 0, prof = 0;
@@ -372,38 +462,74 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     }
     int tmax = act ? N + 6 : 0;
     for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o));
+    tmax = __builtin_amdgcn_readfirstlane(tmax);         // uniform: the chunk loop stays scalar
     if (tmax == 0) return;
-    // inactive lanes walk codeword row 0's decisions (in bounds) and store nothing
-    const int steps = act ? N + 6 : tmax;
-    int smin = steps;
-    for (int o = 32; o > 0; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
-    const uint4 *dq = (const uint4 *)(J.dec + (act ? (int64_t)cw * J.dec_stride : 0));
+    const int steps = act ? N + 6 : 0;                   // inactive lanes walk garbage, store nothing
     uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
-    const int nch = (tmax + TBC - 1) / TBC;
-    auto load = [&](uint4 (&c)[TBC / 2], int ch) {
-        const bool ld = ch >= 0;
-        const uint4 *q = dq + (ld ? ch : 0) * (TBC / 2);
-#pragma unroll
-        for (int k = 0; k < TBC / 2; k++) c[k] = q[k];
-    };
-    auto walk = [&](const uint4 (&c)[TBC / 2], int ch, int &lr, int &rho) {
-        if ((ch + 1) * TBC <= smin) tb_chunk<false>(c, ch, steps, N, lr, rho, act, out, J);
-        else tb_chunk<true>(c, ch, steps, N, lr, rho, act, out, J);
-    };
+    const int nch = (tmax + WS - 1) / WS;
+    const uint32_t *blk0 = J.dec + (int64_t)blockIdx.x * 64 * 64;
+    const int64_t cstride = J.dec_ncw * 64;
     int lr = 0;                                          // lane index holding the traced state
-    int rho = (nch * TBC - 1) % 6;                       // t mod 6 of the step being walked
-    uint4 A[TBC / 2], B[TBC / 2], C[TBC / 2];
-    load(A, nch - 1);
-    load(B, nch - 2);
-    for (int ch = nch - 1; ch >= 0; ch -= 3) {
-        load(C, ch - 2);
-        walk(A, ch, lr, rho);
-        if (ch < 1) break;
-        load(A, ch - 3);
-        walk(B, ch - 1, lr, rho);
-        if (ch < 2) break;
-        load(B, ch - 4);
-        walk(C, ch - 2, lr, rho);
+    // decision chunks stream in through a 3-deep register ring (2 chunks = 32 KB per
+    // wave in flight while one is walked): the walk itself is short, the loads are not
+    u32x4 ra[16], rb[16], rc[16];
+    auto ld = [&](u32x4 (&r)[16], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
+    ld(ra, nch - 1);
+    ld(rb, nch - 2);
+    for (int ch = nch - 1; ch >= 0; ch--) {
+        uint32_t *cur = stage[ch & 1];
+        const int slot = (nch - 1 - ch) % 3;
+        if (slot == 0) { tb_stage(cur, ra, lane); wave_sync(); ld(ra, ch - 3); }
+        else if (slot == 1) { tb_stage(cur, rb, lane); wave_sync(); ld(rb, ch - 3); }
+        else { tb_stage(cur, rc, lane); wave_sync(); ld(rc, ch - 3); }
+        if (ch == nch - 1) ld(rc, ch - 2);
+        const uint32_t *mine = cur + lane * 64;
+        const int t0 = ch * WS;
+        const bool full = t0 + WS <= steps;
+        uint32_t w = 0;                                  // decoded bits of the chunk, step t0+k at bit k
+        // two steps per LDS round trip: with the word of step k, read both candidate
+        // words of step k-1 (the traced lane differs in bit p of step k only)
+        static_assert(WS % 2 == 0, "step pairs");
+#pragma unroll
+        for (int k = WS - 1; k >= 1; k -= 2) {
+            const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);   // relabelling phase of step t0+k is k % 6
+            const uint32_t w1 = mine[lr];
+            const uint32_t c0 = mine[lr & ~(1 << p1)], c1 = mine[lr | (1 << p1)];
+            {
+                const int d = (int)((w1 >> (WS - 1 - k)) & 1u);      // predecessor's msb
+                const int u = (lr >> p1) & 1;                         // decoded bit of step t0 + k
+                const int nl = (lr & ~(1 << p1)) | (d << p1);
+                if (full || t0 + k < steps) {
+                    lr = nl;
+                    w |= (uint32_t)u << k;
+                }
+            }
+            {
+                const uint32_t w2 = ((lr >> p1) & 1) ? c1 : c0;       // = mine[lr]
+                const int d = (int)((w2 >> (WS - k)) & 1u);
+                const int u = (lr >> p2) & 1;
+                const int nl = (lr & ~(1 << p2)) | (d << p2);
+                if (full || t0 + k - 1 < steps) {
+                    lr = nl;
+                    w |= (uint32_t)u << (k - 1);
+                }
+            }
+        }
+        if (act && t0 < N) {
+            if (J.prbs) {                                // energy dispersal bits t0 .. t0+29
+                const int wi = t0 >> 5, sh = t0 & 31;
+                const uint32_t lo = J.prbs_words[wi], hi = J.prbs_words[wi + 1];
+                w ^= sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
+            }
+            if (t0 + WS <= N) {
+#pragma unroll
+                for (int e = 0; e < WS / 2; e++)         // 2 bits -> 2 bytes (t0 is even)
+                    *(uint16_t *)(out + t0 + 2 * e) = (uint16_t)(((w >> (2 * e)) & 1u) | (((w >> (2 * e + 1)) & 1u) << 8));
+            } else {
+                for (int i = 0; t0 + i < N; i++) out[t0 + i] = (uint8_t)((w >> i) & 1u);
+            }
+        }
+        wave_sync();
     }
 }
 
@@ -434,15 +560,21 @@ static hipError_t launch_kind(hipStream_t st, const VitJob &job, dim3 grid) {
     }
     return hipGetLastError();
 }
-template <int KIND> struct AcsK { static auto fn() { return k_acs<KIND>; } };
+template <int KIND> struct AcsK { static auto fn() { return k_acs<KIND, 1>; } };
 template <int KIND> struct TbK { static auto fn() { return k_traceback<KIND>; } };
 
+// One codeword pair per wave (NP = 1).  NP > 1 (independent chains interleaved in one
+// wave, fewer waves) measured slower on MI355X for the C3 batch: 0.81 ms (NP=2) and
+// 1.14 ms (NP=3) vs 0.72 ms per launch -- thread-level parallelism hides the
+// compare -> carry and DPP hazards better than instruction-level parallelism here.
 hipError_t launch_acs(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
-    return launch_kind<AcsK>(st, job, dim3(job.n_cw));
+    if (job.dec_ncw < dec_rows(job.n_cw)) return hipErrorInvalidValue;
+    return launch_kind<AcsK>(st, job, dim3((job.n_cw + 1) / 2));
 }
 hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
+    if (job.dec_ncw < dec_rows(job.n_cw)) return hipErrorInvalidValue;
     return launch_kind<TbK>(st, job, dim3((job.n_cw + 63) / 64));
 }
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {

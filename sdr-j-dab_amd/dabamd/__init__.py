@@ -306,9 +306,13 @@ class Pipeline:
         self.h = h
         self.msc_stride = max([24 * s.bitRate for s in self.subch] + [768])
         self.msc_stride = (self.msc_stride + 15) // 16 * 16
-        self.fic_d = ctx.buf(n_streams * n_frames * 4 * 768)
-        self.crc_d = ctx.buf(n_streams * n_frames * 12)
-        self.msc_d = ctx.buf(max(1, n_streams * 4 * n_frames * len(self.subch) * self.msc_stride))
+        # consecutive runs decode concurrently on two back-end streams (dabgpu.h,
+        # dabgpu_pipe_sync): outputs alternate between two buffer sets
+        self._outs = [(ctx.buf(n_streams * n_frames * 4 * 768), ctx.buf(n_streams * n_frames * 12),
+                       ctx.buf(max(1, n_streams * 4 * n_frames * len(self.subch) * self.msc_stride)))
+                      for _ in range(2)]
+        self._run = 0
+        self.fic_d, self.crc_d, self.msc_d = self._outs[0]
         self.dp = [s for s in self.subch if s.flags & SUBCH_DABPLUS]
         self.sf_stride = max([110 * (s.bitRate // 8) for s in self.dp] + [16])
         if self.dp:
@@ -324,6 +328,8 @@ class Pipeline:
     def run(self, iq: DevBuf, stride: int, n_avail: Sequence[int], download: bool = True):
         na = np.asarray(n_avail, dtype=np.int64)
         valid = np.zeros((self.S, 4 * self.F), dtype=np.uint8)
+        self.fic_d, self.crc_d, self.msc_d = self._outs[self._run & 1]
+        self._run += 1
         _chk(lib().dabgpu_pipe_run(self.h, iq.ptr, stride, _p(na), self.fic_d.ptr, self.crc_d.ptr,
                                    self.msc_d.ptr if self.subch else None, self.msc_stride, _p(valid)),
              "dabgpu_pipe_run")

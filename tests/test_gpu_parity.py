@@ -107,6 +107,33 @@ def test_msc_deconvolve_matches_oracle(ctx):
         assert np.array_equal(outs[i], want), MSC_CASES[i]
 
 
+@pytest.mark.parametrize("seed", [1, 2])
+def test_acs_pairs_mixed_profiles(ctx, seed):
+    """k_acs decodes codewords in pairs (two 16-bit metric halves per lane): a batch
+    mixing profiles and lengths inside a pair, with an odd codeword count (the last
+    pair half empty), against the oracle."""
+    import dabamd
+    np_force = str(seed)
+    rng = np.random.default_rng(100 + seed)
+    cases = [MSC_CASES[i % len(MSC_CASES)] for i in (0, 3, 3, 1, 5, 2, 2, 4, 0, 6, 1)]
+    frags = rng.integers(-127, 128, (len(cases), 27000)).astype(np.int16)
+    subs = [dabamd.Subch(0, 0, br, pl, uepflag, 0) for uepflag, br, pl in cases]
+    outs = ctx.msc_deconvolve(frags, subs)
+    for i, (uepflag, br, pl) in enumerate(cases):
+        want = orc.msc_deconvolve(1 if uepflag == 0 else 0, br, pl, frags[i])
+        assert np.array_equal(outs[i], want), (np_force, i, cases[i])
+    # same-length codewords through the mother-code path, odd count
+    nb = 1000
+    rows = []
+    for i in range(7):
+        bits = rng.integers(0, 2, nb).astype(np.uint8)
+        rows.append(_noisy(rng, _enc(bits), sigma=[0, 80, 160, 240, 320, 120, 400][i]))
+    soft = np.stack(rows)
+    gpu = ctx.viterbi(soft, nb)
+    for i in range(len(rows)):
+        assert np.array_equal(gpu[i], orc.viterbi(soft[i], nb)), (np_force, "mother", i)
+
+
 def test_msc_golden(ctx):
     import os
     import dabamd
