@@ -240,7 +240,9 @@ int dabgpu_pipe_sync(dabgpu_pipe *p);
 #define DABGPU_STAGE_PRS      0   /* k_prs_sync   (findIndex)          */
 #define DABGPU_STAGE_BLOCK0   1   /* k_block0     (processBlock_0 AFC) */
 #define DABGPU_STAGE_DEMOD    2   /* k_demod      (processToken x 75)  */
-#define DABGPU_STAGE_FIC      3   /* FIC Viterbi + CRC                 */
+#define DABGPU_STAGE_FIC      3   /* FIC Viterbi + CRC (CRC only when the run also
+                                     decodes MSC: the FIC's Viterbi then shares the
+                                     MSC's ACS and traceback launches)  */
 #define DABGPU_STAGE_MSC_ACS  4   /* MSC Viterbi add-compare-select    */
 #define DABGPU_STAGE_MSC_TB   5   /* MSC chainback + energy dispersal  */
 #define DABGPU_STAGE_DABPLUS  6   /* k_dabplus (superframe, RS, AU CRC) */

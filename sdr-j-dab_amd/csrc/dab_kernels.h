@@ -130,6 +130,8 @@ hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, i
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
 hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
+hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
 hipError_t launch_rs(hipStream_t st, const uint8_t *in, int n, const uint8_t *tabs, uint8_t *out, int16_t *ret);

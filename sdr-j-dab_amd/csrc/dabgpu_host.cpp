@@ -338,7 +338,13 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     HIPCHK(hipSetDevice(device));
     auto *c = new dabgpu_ctx();
     c->device = device;
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    // the context stream carries the OFDM front end: highest priority, so a streaming
+    // pipeline's next front end takes the SIMDs the Viterbi tail leaves idle
+    {
+        int least = 0, greatest = 0;
+        HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+        HIPCHK(hipStreamCreateWithPriority(&c->stream, hipStreamNonBlocking, greatest));
+    }
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     const HostTables &t = host_tables();
     int rc = 0;
@@ -636,6 +642,7 @@ struct dabgpu_pipe {
     int32_t *slots_d = nullptr;
     uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
     size_t dec_sz = 0;
+    int64_t dec_fic_off = 0;                    // FIC decisions: words after the MSC's
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
     std::vector<int32_t> last_si;
@@ -748,13 +755,17 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->fc_d, sizeof(float2) * SF);
     A((void **)&p->fcpart_d, sizeof(float2) * SF * kMaxChunks);
     A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
-    const size_t ncw = std::max(SF * 4 * std::max(p->NSUB, 1), SF * 4);
-    p->dec_sz = (size_t)std::max(dec_bytes((int)ncw, p->max_nbits), dec_bytes(SF * 4, 768));
+    // MSC decisions, then the FIC's (both jobs of one run decode in one launch)
+    const int64_t msc_words = p->NSUB > 0 ? dec_bytes(SF * 4 * p->NSUB, p->max_nbits) / 4 : 0;
+    p->dec_fic_off = msc_words;
+    p->dec_sz = (size_t)(4 * msc_words + dec_bytes(SF * 4, 768));
     A((void **)&p->dec_d[0], p->dec_sz);
     A((void **)&p->dec_d[1], p->dec_sz);
     A((void **)&p->ficprof_d, sizeof(Profile));
-    if (!rc && (hipStreamCreateWithFlags(&p->vs[0], hipStreamNonBlocking) != hipSuccess ||
-                hipStreamCreateWithFlags(&p->vs[1], hipStreamNonBlocking) != hipSuccess ||
+    int prio_least = 0, prio_greatest = 0;
+    if (!rc && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) rc = fail(DABGPU_E_HIP, "priority range");
+    if (!rc && (hipStreamCreateWithPriority(&p->vs[0], hipStreamNonBlocking, prio_least) != hipSuccess ||
+                hipStreamCreateWithPriority(&p->vs[1], hipStreamNonBlocking, prio_least) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_dp, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_front, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_back[0], hipEventDisableTiming) != hipSuccess ||
@@ -1102,64 +1113,76 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     hipStream_t bs = p->vs[par];
     HIPCHK(hipEventRecord(p->ev_front, c->stream));
     HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
-    // FIC for every committed frame
-    {
+    // FIC for every committed frame, MSC for all subchannels of all CIFs of this run.
+    // With both, one ACS and one traceback launch decode them together (the FIC's short
+    // waves fill the SIMDs the MSC's last waves leave idle); decisions in separate
+    // halves of this stream's decision buffer.
+    const int64_t cif0 = p->st[0].cif_count;
+    const bool do_msc = msc_bits && p->NSUB > 0 && all;
+    if (do_msc && msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
+    VitJob JF, JM;
+    memset(&JF, 0, sizeof JF);
+    memset(&JM, 0, sizeof JM);
+    if (fic_bits) {
         std::vector<int32_t> slots((size_t)S * F);
         for (int s = 0; s < S; s++)
             for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = p->last_frames[(size_t)s * F + f].out_slot;
-        if (fic_bits) {
-            int32_t *slots_d = p->slots_d + (size_t)par * S * F;
-            HIPCHK(hipMemcpyAsync(slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, bs));
-            void *pd = p->ficprof_d;
-            VitJob J;
-            memset(&J, 0, sizeof J);
-            J.kind = SRC_FIC;
-            J.n_cw = 4 * S * F;
-            J.src = p->ring;
-            J.src_len = (int64_t)S * p->R * FRAME_SOFT;
-            J.err = c->err;
-            J.slots = slots_d;
-            J.prof = (const Profile *)pd;
-            J.out = fic_bits;
-            J.out_stride = 768;
-            J.prbs = 1;
-            J.prbs_words = c->prbs;
-            J.dec = p->dec_d[par];
-            J.dec_ncw = dec_rows(J.n_cw);
-            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-            HIPCHK(launch_viterbi(bs, J));
-            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F));
-            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
-        }
+        int32_t *slots_d = p->slots_d + (size_t)par * S * F;
+        HIPCHK(hipMemcpyAsync(slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, bs));
+        JF.kind = SRC_FIC;
+        JF.n_cw = 4 * S * F;
+        JF.src = p->ring;
+        JF.src_len = (int64_t)S * p->R * FRAME_SOFT;
+        JF.err = c->err;
+        JF.slots = slots_d;
+        JF.prof = (const Profile *)p->ficprof_d;
+        JF.out = fic_bits;
+        JF.out_stride = 768;
+        JF.prbs = 1;
+        JF.prbs_words = c->prbs;
+        JF.dec = p->dec_d[par] + p->dec_fic_off;
+        JF.dec_ncw = dec_rows(JF.n_cw);
     }
-    // MSC: all subchannels of all CIFs of this run
-    const int64_t cif0 = p->st[0].cif_count;
-    if (msc_bits && p->NSUB > 0 && all) {
-        if (msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
-        VitJob J;
-        memset(&J, 0, sizeof J);
-        J.kind = SRC_MSC;
-        J.n_cw = S * 4 * F * p->NSUB;
-        J.src = p->ring;
-        J.src_len = (int64_t)S * p->R * FRAME_SOFT;
-        J.err = c->err;
-        J.prof = p->prof_d;
-        J.nsub = p->NSUB;
-        J.ncif = 4 * F;
-        J.ring = p->R;
-        J.cif0 = cif0;
-        J.sub_start = p->substart_d;
-        J.out = msc_bits;
-        J.out_stride = msc_stride;
-        J.prbs = 1;
-        J.prbs_words = c->prbs;
-        J.dec = p->dec_d[par];
-        J.dec_ncw = dec_rows(J.n_cw);
+    if (do_msc) {
+        JM.kind = SRC_MSC;
+        JM.n_cw = S * 4 * F * p->NSUB;
+        JM.src = p->ring;
+        JM.src_len = (int64_t)S * p->R * FRAME_SOFT;
+        JM.err = c->err;
+        JM.prof = p->prof_d;
+        JM.nsub = p->NSUB;
+        JM.ncif = 4 * F;
+        JM.ring = p->R;
+        JM.cif0 = cif0;
+        JM.sub_start = p->substart_d;
+        JM.out = msc_bits;
+        JM.out_stride = msc_stride;
+        JM.prbs = 1;
+        JM.prbs_words = c->prbs;
+        JM.dec = p->dec_d[par];
+        JM.dec_ncw = dec_rows(JM.n_cw);
+    }
+    if (fic_bits && do_msc) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs(bs, J));
+        HIPCHK(launch_acs_msc_fic(bs, JM, JF));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
-        HIPCHK(launch_traceback(bs, J));
+        HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
+        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
+    } else if (fic_bits) {
+        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
+        HIPCHK(launch_viterbi(bs, JF));
+        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
+    } else if (do_msc) {
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
+        HIPCHK(launch_acs(bs, JM));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
+        HIPCHK(launch_traceback(bs, JM));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
     }
     HIPCHK(hipEventRecord(p->ev_back[par], bs));

@@ -334,13 +334,17 @@ __device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&ro
     for (int p = 0; p < NP; p++) x[p] = renorm(x[p]);
 }
 
-// NP pairs of codewords per wave: codewords 2*NP*w .. 2*NP*w + 2*NP - 1 (logical order)
+// NP pairs of codewords per wave: codewords 2*NP*w .. 2*NP*w + 2*NP - 1 (logical order).
+// LDS (kernel-owned, so two jobs in one launch share it): bm[NP*8*BRS], rowoff[2*NP][16]
+template <int NP> struct AcsLds {
+    uint32_t bm[NP * 8 * BRS];
+    int32_t rowoff[2 * NP][16];
+};
 template <int KIND, int NP>
-__global__ __launch_bounds__(64, 8) void k_acs(VitJob J) {
-    __shared__ uint32_t bm[NP * 8 * BRS];
-    __shared__ int32_t rowoff[2 * NP][16];
+__device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) {
+    uint32_t *bm = L.bm;
+    int32_t (*rowoff)[16] = L.rowoff;
     const int lane = threadIdx.x;
-    const int w = xcd_order(blockIdx.x, gridDim.x);
     Src c[2 * NP];
     bool any = false;
 #pragma unroll
@@ -442,9 +446,11 @@ __device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[16], in
 }
 
 template <int KIND>
-__global__ __launch_bounds__(64) void k_traceback(VitJob J) {
-    __shared__ uint32_t stage[2][TB_WORDS];
-    const int lane = threadIdx.x, cw = blockIdx.x * 64 + lane;
+__device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*stage)[TB_WORDS]) {
+    // a latency-bound chain that issues little: first pick on its SIMD, so it keeps
+    // its pace next to throughput-bound waves of other kernels (the next run's demod)
+    __builtin_amdgcn_s_setprio(3);
+    const int lane = threadIdx.x, cw = blk * 64 + lane;
     bool act = cw < J.n_cw;
     int N = 0, prof = 0;
     if (act) {
@@ -467,7 +473,7 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     const int steps = act ? N + 6 : 0;                   // inactive lanes walk garbage, store nothing
     uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
     const int nch = (tmax + WS - 1) / WS;
-    const uint32_t *blk0 = J.dec + (int64_t)blockIdx.x * 64 * 64;
+    const uint32_t *blk0 = J.dec + (int64_t)blk * 64 * 64;
     const int64_t cstride = J.dec_ncw * 64;
     int lr = 0;                                          // lane index holding the traced state
     // decision chunks stream in through a 3-deep register ring (2 chunks = 32 KB per
@@ -533,6 +539,32 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     }
 }
 
+template <int KIND>
+__global__ __launch_bounds__(64, 8) void k_acs(VitJob J) {
+    __shared__ AcsLds<1> L;
+    acs_body<KIND, 1>(J, xcd_order(blockIdx.x, gridDim.x), L);
+}
+// two jobs in one launch (the pipeline's MSC and FIC): blocks [0, nwa) run job A,
+// the rest job B, so B's short waves fill the SIMDs A's last waves leave idle
+template <int KA, int KB>
+__global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
+    __shared__ AcsLds<1> L;
+    const int b = blockIdx.x;
+    if (b < nwa) acs_body<KA, 1>(A, xcd_order(b, nwa), L);
+    else acs_body<KB, 1>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
+}
+template <int KIND>
+__global__ __launch_bounds__(64) void k_traceback(VitJob J) {
+    __shared__ uint32_t stage[2][TB_WORDS];
+    tb_body<KIND>(J, blockIdx.x, stage);
+}
+template <int KA, int KB>
+__global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) {
+    __shared__ uint32_t stage[2][TB_WORDS];
+    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, stage);
+    else tb_body<KB>(B, blockIdx.x - nba, stage);
+}
+
 // FIB CRC check (dab-constants.h:310-340): invert the 16 CRC bits in place, run
 // CRC-CCITT from all-ones over 256 bits, pass iff the register ends at zero.
 __global__ void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok, int n_fib) {
@@ -560,7 +592,7 @@ static hipError_t launch_kind(hipStream_t st, const VitJob &job, dim3 grid) {
     }
     return hipGetLastError();
 }
-template <int KIND> struct AcsK { static auto fn() { return k_acs<KIND, 1>; } };
+template <int KIND> struct AcsK { static auto fn() { return k_acs<KIND>; } };
 template <int KIND> struct TbK { static auto fn() { return k_traceback<KIND>; } };
 
 // One codeword pair per wave (NP = 1).  NP > 1 (independent chains interleaved in one
@@ -580,6 +612,20 @@ hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     hipError_t e = launch_acs(st, job);
     return e != hipSuccess ? e : launch_traceback(st, job);
+}
+// MSC (a) and FIC (b) decoded by one ACS launch and one traceback launch
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+    if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
+    if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw)) return hipErrorInvalidValue;
+    const int nwa = (a.n_cw + 1) / 2, nwb = (b.n_cw + 1) / 2;
+    hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
+    return hipGetLastError();
+}
+hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+    if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
+    const int nba = (a.n_cw + 63) / 64, nbb = (b.n_cw + 63) / 64;
+    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(nba + nbb), dim3(64), 0, st, a, b, nba);
+    return hipGetLastError();
 }
 
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib) {
