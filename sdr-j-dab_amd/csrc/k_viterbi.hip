@@ -433,7 +433,10 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 // reads word [l][lr] where lr is the lane that held its traced state.  A chunk is
 // one word of WS steps starting at relabelling phase 0, so the bit positions and the
 // phase of every step are compile-time constants.
-constexpr int TB_WORDS = 64 * 64;          // one chunk of a wave's 64 codewords
+// LDS row per codeword: 64 words + 1 pad, so lanes tracing the same state (equal
+// lr, common when the streams carry similar data) read 64 different banks
+constexpr int TB_ROW = 65;
+constexpr int TB_WORDS = 64 * TB_ROW;      // one chunk of a wave's 64 codewords
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 copies as a memcpy -> scratch)
 __device__ __forceinline__ void tb_load(u32x4 (&r)[16], const uint32_t *blk, int lane) {
     const u32x4 *q = (const u32x4 *)blk;
@@ -441,8 +444,16 @@ __device__ __forceinline__ void tb_load(u32x4 (&r)[16], const uint32_t *blk, int
     for (int i = 0; i < 16; i++) r[i] = q[i * 64 + lane];
 }
 __device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[16], int lane) {
+    // r[i] = words 4q..4q+3 of the linear [64][64] block, q = i*64 + lane
 #pragma unroll
-    for (int i = 0; i < 16; i++) ((u32x4 *)lds)[i * 64 + lane] = r[i];
+    for (int i = 0; i < 16; i++) {
+        const int q = i * 64 + lane, row = q >> 4, col = (q & 15) * 4;
+        uint32_t *d = lds + row * TB_ROW + col;
+        d[0] = r[i].x;
+        d[1] = r[i].y;
+        d[2] = r[i].z;
+        d[3] = r[i].w;
+    }
 }
 
 template <int KIND>
@@ -471,6 +482,9 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     tmax = __builtin_amdgcn_readfirstlane(tmax);         // uniform: the chunk loop stays scalar
     if (tmax == 0) return;
     const int steps = act ? N + 6 : 0;                   // inactive lanes walk garbage, store nothing
+    int smin = act ? steps : tmax;                       // chunks below smin are whole in every lane
+    for (int o = 32; o > 0; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
+    smin = __builtin_amdgcn_readfirstlane(smin);
     uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
     const int nch = (tmax + WS - 1) / WS;
     const uint32_t *blk0 = J.dec + (int64_t)blk * 64 * 64;
@@ -489,35 +503,54 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
         else if (slot == 1) { tb_stage(cur, rb, lane); wave_sync(); ld(rb, ch - 3); }
         else { tb_stage(cur, rc, lane); wave_sync(); ld(rc, ch - 3); }
         if (ch == nch - 1) ld(rc, ch - 2);
-        const uint32_t *mine = cur + lane * 64;
+        const uint32_t *mine = cur + lane * TB_ROW;
         const int t0 = ch * WS;
-        const bool full = t0 + WS <= steps;
         uint32_t w = 0;                                  // decoded bits of the chunk, step t0+k at bit k
         // two steps per LDS round trip: with the word of step k, read both candidate
         // words of step k-1 (the traced lane differs in bit p of step k only)
         static_assert(WS % 2 == 0, "step pairs");
+        if (t0 + WS <= smin) {
+            // every lane's chunk is whole: straight bit arithmetic, no per-step checks.
+            // m = -(decision) as a 0 / all-ones mask: lr's bit p := d is one bfi, and
+            // the candidate of step k-1 is picked bitwise by the same mask.
 #pragma unroll
-        for (int k = WS - 1; k >= 1; k -= 2) {
-            const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);   // relabelling phase of step t0+k is k % 6
-            const uint32_t w1 = mine[lr];
-            const uint32_t c0 = mine[lr & ~(1 << p1)], c1 = mine[lr | (1 << p1)];
-            {
-                const int d = (int)((w1 >> (WS - 1 - k)) & 1u);      // predecessor's msb
-                const int u = (lr >> p1) & 1;                         // decoded bit of step t0 + k
-                const int nl = (lr & ~(1 << p1)) | (d << p1);
-                if (full || t0 + k < steps) {
-                    lr = nl;
-                    w |= (uint32_t)u << k;
-                }
+            for (int k = WS - 1; k >= 1; k -= 2) {
+                const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);   // phase of step t0+k is k % 6
+                const uint32_t b1 = 1u << p1, b2 = 1u << p2;
+                const uint32_t w1 = mine[lr], c0 = mine[lr & ~b1], c1 = mine[lr | b1];
+                const uint32_t m1 = (uint32_t)((int32_t)(w1 << (32 - WS + k)) >> 31); // -(bit WS-1-k)
+                w |= (k >= p1 ? ((uint32_t)lr << (k - p1)) : ((uint32_t)lr >> (p1 - k))) & (1u << k);
+                lr = (int)((m1 & b1) | ((uint32_t)lr & ~b1));
+                const uint32_t w2 = (m1 & c1) | (~m1 & c0);
+                const uint32_t m2 = (uint32_t)((int32_t)(w2 << (32 - WS + k - 1)) >> 31);
+                w |= ((k - 1) >= p2 ? ((uint32_t)lr << (k - 1 - p2)) : ((uint32_t)lr >> (p2 - k + 1))) & (1u << (k - 1));
+                lr = (int)((m2 & b2) | ((uint32_t)lr & ~b2));
             }
-            {
-                const uint32_t w2 = ((lr >> p1) & 1) ? c1 : c0;       // = mine[lr]
-                const int d = (int)((w2 >> (WS - k)) & 1u);
-                const int u = (lr >> p2) & 1;
-                const int nl = (lr & ~(1 << p2)) | (d << p2);
-                if (full || t0 + k - 1 < steps) {
-                    lr = nl;
-                    w |= (uint32_t)u << (k - 1);
+        } else {
+            const bool full = t0 + WS <= steps;
+#pragma unroll
+            for (int k = WS - 1; k >= 1; k -= 2) {
+                const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);
+                const uint32_t w1 = mine[lr];
+                const uint32_t c0 = mine[lr & ~(1 << p1)], c1 = mine[lr | (1 << p1)];
+                {
+                    const int d = (int)((w1 >> (WS - 1 - k)) & 1u);  // predecessor's msb
+                    const int u = (lr >> p1) & 1;                     // decoded bit of step t0 + k
+                    const int nl = (lr & ~(1 << p1)) | (d << p1);
+                    if (full || t0 + k < steps) {
+                        lr = nl;
+                        w |= (uint32_t)u << k;
+                    }
+                }
+                {
+                    const uint32_t w2 = ((lr >> p1) & 1) ? c1 : c0;   // = mine[lr]
+                    const int d = (int)((w2 >> (WS - k)) & 1u);
+                    const int u = (lr >> p2) & 1;
+                    const int nl = (lr & ~(1 << p2)) | (d << p2);
+                    if (full || t0 + k - 1 < steps) {
+                        lr = nl;
+                        w |= (uint32_t)u << (k - 1);
+                    }
                 }
             }
         }
