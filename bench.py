@@ -156,7 +156,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--ensembles", type=int, default=0, help="ensembles per GPU (default: C3 64, C5 16)")
-    ap.add_argument("--frames", type=int, default=8, help="frames per ensemble per step")
+    ap.add_argument("--frames", type=int, default=24,
+                    help="frames per ensemble per step (the pipeline's batch: 24 frames = 2.3 s of air time; "
+                         "throughput saturates from ~24 on MI355X, profiles/r01_frames_sweep.txt)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()

@@ -1,0 +1,70 @@
+// valu_rate.hip -- calibration microbenchmark (not part of the product): sustained
+// wave64 VALU issue rate per SIMD on this GPU for the instruction classes k_acs uses
+// (32-bit add, packed 16-bit add/min, DPP move, 16-bit compare into a lane mask).
+// Grid: 32 waves per CU (8 per SIMD), each with 8 independent dependency chains.
+// Prints cycles per wave-instruction per SIMD (2.0 = full rate of a SIMD-32).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdint>
+#define CK(x) (void)(x)
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+template <int OP>
+__global__ __launch_bounds__(64) void k_rate(uint32_t *out, int iters) {
+    uint32_t v[8];
+    const uint32_t k1 = threadIdx.x * 7 + 1;
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = threadIdx.x * 13 + c;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                if constexpr (OP == 0) asm volatile("v_add_u32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 1) asm volatile("v_pk_add_u16 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 2) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf" : "+v"(v[c]));
+                else if constexpr (OP == 3) asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 4) asm volatile("v_cmp_gt_u16_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:WORD_1" :: "v"(v[c]), "v"(k1) : "vcc");
+            }
+        }
+    }
+    uint32_t s = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) s ^= v[c];
+    out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+template <int OP>
+static void run(const char *name, int cus) {
+    const int waves = cus * 32, iters = 2000;
+    uint32_t *d;
+    CK(hipMalloc(&d, sizeof(uint32_t) * waves * 64));
+    hipEvent_t a, b;
+    hipEventCreate(&a);
+    hipEventCreate(&b);
+    hipLaunchKernelGGL(k_rate<OP>, dim3(waves), dim3(64), 0, 0, d, 10);
+    hipEventRecord(a);
+    hipLaunchKernelGGL(k_rate<OP>, dim3(waves), dim3(64), 0, 0, d, iters);
+    hipEventRecord(b);
+    hipEventSynchronize(b);
+    float ms = 0;
+    hipEventElapsedTime(&ms, a, b);
+    int clk_khz = 0;
+    hipDeviceGetAttribute(&clk_khz, hipDeviceAttributeClockRate, 0);
+    const double instrs_per_simd = (double)8 /*waves per SIMD*/ * iters * 16 * 8;
+    const double cycles = ms * 1e-3 * clk_khz * 1e3;
+    printf("%-28s %8.3f ms  %.2f cycles per wave-instruction per SIMD (clock %.2f GHz)\n", name, ms,
+           cycles / instrs_per_simd, clk_khz / 1e6);
+    hipFree(d);
+}
+
+int main() {
+    int cus = 0;
+    hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
+    run<0>("v_add_u32", cus);
+    run<1>("v_pk_add_u16", cus);
+    run<2>("v_mov_b32_dpp quad_perm", cus);
+    run<3>("v_pk_min_u16", cus);
+    run<4>("v_cmp_gt_u16_sdwa", cus);
+    return 0;
+}
