@@ -11,9 +11,6 @@ constexpr int NSYM = 75;                 // data symbols per frame
 constexpr int SYMBITS = 2 * K;           // 3072 soft bits per symbol
 constexpr int FRAME_SOFT = NSYM * SYMBITS;
 constexpr int INPUT_RATE = 2048000;
-// k_demod keeps, per lane (k1 = lane>>1, r = lane&1), only the FFT slots that hold
-// carriers +-1..768: k2 = j + 8r for j < DEMOD_NPJ (r=0: bins 0..799, r=1: 1280..2047)
-constexpr int DEMOD_NPJ = 25;            // (cmap_l holds (DEMOD_NPJ + 1) / 2 words per lane)
 
 // device tables for the OFDM kernels (built on the host with the reference's
 // own float expressions, see dabgpu.cpp: make_tables)
@@ -21,8 +18,9 @@ struct OfdmTables {
     const float2 *osc;      // oscillatorTable[2048000] (ofdm-processor.cpp:79-81)
     const float2 *tw;       // twiddle bases [12][64]: rows a=0..7 W2048^{n2*a}, rows 8+b W2048^{n2*8b}
     const float2 *ref_l;    // PRS refTable in FFT output lane layout [i][lane]
-    const uint32_t *cmap_l; // carrier of compact slot j (k2 = j + 8r) [j/2][lane], two int16 per word (-1 unused)
     const float *refarg;    // refArg[18] (ofdm-decoder.cpp:71-74)
+    const float2 *w2048;    // W2048^j = e^{-2 pi i j/2048}, j < 2048 (double, rounded to float)
+    const int16_t *carrier_of_bin;   // [2048] carrier index of an FFT bin (mapper.cpp), -1 if none
     int32_t *err;           // device error word: kernels OR in DABGPU_KERR_* bits
 };
 constexpr int KERR_FRAME = 1;      // frame descriptor outside its stream / bad NCO phase

@@ -63,7 +63,9 @@ float get_phi(int k) {                                   // phasetable.cpp:261-2
 
 struct HostTables {
     std::vector<float2> osc, tw, ref_l;
-    std::vector<uint32_t> cmap_l, prbs_words;
+    std::vector<uint32_t> prbs_words;
+    std::vector<float2> w2048;
+    std::vector<int16_t> carrier_bin;
     std::vector<float> refarg;
     std::vector<float2> ref;                // natural order refTable
     std::vector<int16_t> perm;              // carrier -> signed carrier (mapIn)
@@ -102,22 +104,16 @@ struct HostTables {
         std::vector<int> carrier_of_bin(2048, -1);
         for (int c = 0; c < 1536; c++) { int k = perm[c]; carrier_of_bin[k < 0 ? k + 2048 : k] = c; }
         ref_l.resize(32 * 64);
-        cmap_l.assign((DEMOD_NPJ + 1) / 2 * 64, 0u);
         for (int lane = 0; lane < 64; lane++) {
             int k1 = lane >> 1, r = lane & 1;
             for (int i = 0; i < 32; i++) ref_l[i * 64 + lane] = ref[k1 + 32 * brev5h(i) + 1024 * r];
-            // compact slot j <-> k2 = j + 8r: the bins of carriers +-1..768 (k_demod)
-            for (int j = 0; j < (DEMOD_NPJ + 1) / 2 * 2; j++) {
-                const int k2 = j + 8 * r;
-                const int c = k2 < 32 ? carrier_of_bin[k1 + 32 * k2 + 1024 * r] : -1;
-                const uint32_t w = (uint32_t)(uint16_t)(int16_t)c;
-                cmap_l[(j >> 1) * 64 + lane] |= (j & 1) ? w << 16 : w;
-            }
         }
-        for (int b = 0; b < 2048; b++) {      // every carrier bin lies in some lane's compact slots
-            const int k1 = b & 31, k2 = (b >> 5) & 31, r = b >> 10;
-            if (carrier_of_bin[b] >= 0 && (k2 - 8 * r < 0 || k2 - 8 * r >= DEMOD_NPJ)) abort();
-            (void)k1;
+        carrier_bin.resize(2048);              // k_demod: carrier of each FFT bin
+        for (int b = 0; b < 2048; b++) carrier_bin[b] = (int16_t)carrier_of_bin[b];
+        w2048.resize(2048);                    // k_demod twiddles
+        for (int j = 0; j < 2048; j++) {
+            const double ph = -2.0 * M_PI * j / 2048.0;
+            w2048[j] = make_float2((float)cos(ph), (float)sin(ph));
         }
         refarg.resize(18);
         for (int i = 0; i < 18; i++) {        // ofdm-decoder.cpp:71-74
@@ -272,7 +268,9 @@ struct dabgpu_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[16] = {};
     float2 *osc = nullptr, *tw = nullptr, *ref_l = nullptr;
-    uint32_t *cmap_l = nullptr, *prbs = nullptr;
+    uint32_t *prbs = nullptr;
+    float2 *w2048 = nullptr;
+    int16_t *carrier_bin = nullptr;
     float *refarg = nullptr;
     uint8_t *dptab = nullptr;    // DAB+ tables (HostTables::dptab)
     int32_t *err = nullptr;      // device error word (KERR_* bits)
@@ -349,7 +347,8 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     const HostTables &t = host_tables();
     int rc = 0;
     if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->tw, t.tw)) || (rc = upload(c, &c->ref_l, t.ref_l)) ||
-        (rc = upload(c, &c->cmap_l, t.cmap_l)) || (rc = upload(c, &c->prbs, t.prbs_words)) ||
+        (rc = upload(c, &c->w2048, t.w2048)) || (rc = upload(c, &c->carrier_bin, t.carrier_bin)) ||
+        (rc = upload(c, &c->prbs, t.prbs_words)) ||
         (rc = upload(c, &c->refarg, t.refarg)) || (rc = upload(c, &c->dptab, t.dptab))) {
         dabgpu_ctx_destroy(c);
         return rc;
@@ -357,7 +356,8 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     c->T.osc = c->osc;
     c->T.tw = c->tw;
     c->T.ref_l = c->ref_l;
-    c->T.cmap_l = c->cmap_l;
+    c->T.w2048 = c->w2048;
+    c->T.carrier_of_bin = c->carrier_bin;
     c->T.refarg = c->refarg;
     if (hipMalloc((void **)&c->err, sizeof(int32_t)) != hipSuccess || hipMemset(c->err, 0, sizeof(int32_t)) != hipSuccess) {
         dabgpu_ctx_destroy(c);
@@ -372,7 +372,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->cmap_l, (void *)c->prbs,
+    for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
                     (void *)c->refarg, (void *)c->err, (void *)c->dptab})
         if (p) (void)hipFree(p);
     for (auto p : c->scratch) if (p) (void)hipFree(p);
@@ -444,18 +444,29 @@ int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n,
     HIPCHK(launch_block0(c->stream, iq, fr, n, c->T, corr, true));
     return 0;
 }
-// symbols 1..75 of a frame are split over `chunks` waves (each recomputes the FFT
-// of the symbol before its first one): enough waves to fill 256 CUs several
-// times over, at most 25 (3 symbols per wave).
+// symbols 1..75 of a frame are split over `chunks` workgroups of k_demod (each
+// recomputes the FFT of the symbol before its first one).  Pick the split whose
+// rounds of resident workgroups (kDemodWgPerCu per CU) cost least:
+// rounds * (symbols per chunk + 1 warm-up symbol).
 static const int kMaxChunks = 25;
+static const int kDemodWgPerCu = 3;
 static int demod_chunks(int n) {
-    static const int div[] = {3, 5, 15, 25};
-    int c = 3;
-    for (int d : div) {
-        c = d;
-        if ((int64_t)n * d >= 6144) break;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            cus = 256;
+        cus = std::max(cus, 1);
     }
-    return c;
+    const int64_t slots = (int64_t)kDemodWgPerCu * cus;
+    int best = 1;
+    double best_cost = 1e30;
+    for (int c : {1, 2, 3, 5, 15, 25}) {
+        const int64_t items = (int64_t)n * c;
+        const double cost = (double)((items + slots - 1) / slots) * ((NSYM + c - 1) / c + 1);
+        if (cost < best_cost - 1e-9) { best_cost = cost; best = c; }
+    }
+    return best;
 }
 static int demod_impl(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t *soft, float *softf,
                       float *fc, bool general) {

@@ -1,21 +1,13 @@
 // k_ofdm.hip -- OFDM front-end kernels for gfx950 (one wave64 per work item):
 //   k_prs_sync : phaseReference::findIndex   (phasereference.cpp:60-88)
 //   k_block0   : ofdmDecoder::processBlock_0 (ofdm-decoder.cpp:85-127, method 1)
-//   k_demod    : ofdmDecoder::processToken x 75 per frame (ofdm-decoder.cpp:167-190)
-//                + the FreqCorr guard correlation (ofdm-processor.cpp:424-438)
+//   (k_demod, processToken x 75 + FreqCorr: k_demod.hip)
 //   k_acquire  : ofdmProcessor::run notSynced..SyncOnEndNull (ofdm-processor.cpp:274-338)
 // Every sample read applies the getSamples NCO (ofdm-processor.cpp:217-226).
 #include "dab_device.h"
 #include "dab_kernels.h"
 
 namespace dab {
-
-#ifndef DEMOD_WAVES
-#define DEMOD_WAVES 2          // waves per SIMD the register budget is sized for
-#endif
-#ifndef DEMOD_WG
-#define DEMOD_WG 4             // independent waves per workgroup (share the twiddle table)
-#endif
 
 // sample j (1-based count inside a getSamples segment that started with
 // localPhase lp0): oscillatorTable[(lp0 - j*phase) mod 2048000]
@@ -171,104 +163,6 @@ __global__ __launch_bounds__(64) void k_block0(const float2 *__restrict__ iq,
     if (lane == 0) correction[f] = (int16_t)(bidx - 36);
 }
 
-// compact FFT slot j of this lane: k2 = j + 8r (see DEMOD_NPJ)
-template <int J>
-__device__ __forceinline__ float2 cslot(const float2 (&v)[32], bool r) {
-    const float2 a = v[brev5(J)];
-    if constexpr (J + 8 < 32) {
-        const float2 b = v[brev5(J + 8)];
-        constexpr uint64_t ODD = 0xAAAAAAAAAAAAAAAAull;       // lanes with r = 1
-        return make_float2(sel_lanes<ODD>(a.x, b.x), sel_lanes<ODD>(a.y, b.y));
-    } else {
-        return a;                                   // r = 1: no carrier (cmap -1)
-    }
-}
-
-// One wave per (frame, chunk of symbols).  Registers: the symbol being transformed
-// (32 float2) and the previous symbol's spectrum compacted to the DEMOD_NPJ slots
-// that hold carriers (25 float2); LDS: the fft2048 half-transpose scratch, reused
-// to stage the int16 soft bits for one coalesced 6 KB store per symbol.
-template <bool GEN>
-__global__ __launch_bounds__(64 * DEMOD_WG, DEMOD_WAVES) void k_demod(const float2 *__restrict__ iq,
-                                              const dabgpu_frame *__restrict__ frames, int nitems, int nchunks,
-                                              OfdmTables T, int16_t *__restrict__ soft,
-                                              float *__restrict__ softf, float2 *__restrict__ fcpart) {
-    __shared__ float2 lds_all[DEMOD_WG * FFT_LDS_FLOAT2 + 12 * 64];
-    static_assert(FFT_LDS_FLOAT2 * 8 >= 2 * (2 * K + 128), "soft-bit staging fits the FFT scratch");
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    float2 *twl = lds_all + DEMOD_WG * FFT_LDS_FLOAT2;
-    for (int i = threadIdx.x; i < 12 * 64; i += 64 * DEMOD_WG) twl[i] = T.tw[i];
-    __syncthreads();
-    const int item = blockIdx.x * DEMOD_WG + wv;
-    if (item >= nitems) return;
-    float2 *lds = lds_all + wv * FFT_LDS_FLOAT2;
-    const int fi = item / nchunks, ch = item % nchunks;
-    const dabgpu_frame fr = frames[fi];
-    const float2 *s = iq + fr.iq_base;
-    const int per = (NSYM + nchunks - 1) / nchunks;
-    const int l0 = 1 + ch * per, l1 = min(NSYM + 1, l0 + per);
-    const bool r = lane & 1;
-    float2 fc = make_float2(0.0f, 0.0f);
-    if (l0 <= NSYM && frame_ok(fr, fr.block0 + TU + (int64_t)NSYM * TS, T.err)) {
-        const int64_t dorg = fr.block0 + TU;       // first sample of segment B
-        TwiddlesLds tw{twl + lane};
-        float2 X[32], P[DEMOD_NPJ];
-        if (l0 == 1) load_mixed<GEN>(s, fr.block0, fr.lp_window, fr.phase_a, fr.window, T.osc, X, lane);
-        else load_mixed<GEN>(s, fr.block0 + (int64_t)(l0 - 1) * TS, fr.lp_data, fr.phase_b, dorg, T.osc, X, lane);
-        fft2048(X, lds, tw, lane);
-        sfor<0, DEMOD_NPJ>([&](auto jc) { P[decltype(jc)::value] = cslot<decltype(jc)::value>(X, r); });
-        for (int l = l0; l < l1; l++) {
-            const int64_t u0 = fr.block0 + (int64_t)l * TS;
-            load_mixed<GEN>(s, u0, fr.lp_data, fr.phase_b, dorg, T.osc, X, lane);
-            {
-                float2 g[8];
-                load_mixed<GEN>(s, u0 - 512, fr.lp_data, fr.phase_b, dorg, T.osc, g, lane);
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    if (q > 0 || lane >= 8) {
-                        float2 p = cmul_conj_exact(X[24 + q], g[q]);
-                        fc.x += p.x; fc.y += p.y;
-                    }
-                }
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            fft2048(X, lds, tw, lane);
-            __builtin_amdgcn_sched_barrier(0);
-            int16_t *st = (int16_t *)lds;
-            float *sf = softf ? softf + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS : nullptr;
-            uint32_t cpair = 0;
-            sfor<0, DEMOD_NPJ>([&](auto jc) {
-                constexpr int j = decltype(jc)::value;
-                if constexpr ((j & 1) == 0) cpair = T.cmap_l[(j >> 1) * 64 + lane];
-                const int c = (int)(int16_t)((j & 1) ? (cpair >> 16) : (cpair & 0xFFFFu));
-                const float2 x = cslot<j>(X, r);
-                const float2 r1 = cmul_conj_exact(x, P[j]);
-                P[j] = x;
-                const float ab = fabsf(r1.x) + fabsf(r1.y);
-                const float qr = -r1.x / ab, qi = -r1.y / ab;
-                // unused slot -> dummy LDS words past the 2K soft bits
-                st[c >= 0 ? c : 2 * K + lane] = (int16_t)trunc127(qr);
-                st[c >= 0 ? K + c : 2 * K + 64 + lane] = (int16_t)trunc127(qi);
-                if (sf && c >= 0) { sf[c] = qr; sf[K + c] = qi; }
-                if constexpr ((j & 3) == 3) __builtin_amdgcn_sched_barrier(0);
-            });
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            int4 *dst = (int4 *)(soft + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS);
-            const int4 *src = (const int4 *)st;
-#pragma unroll
-            for (int i = 0; i < 6; i++) dst[lane + 64 * i] = src[lane + 64 * i];
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        }
-    }
-    fc.x = wave_sum(fc.x);
-    fc.y = wave_sum(fc.y);
-    if (lane == 0) fcpart[item] = fc;
-}
-
 // ---- acquisition: one thread per stream runs the reference's sequential
 // null search exactly (double-precision sLevel IIR, float envelope sums).
 __device__ __forceinline__ float jan_abs(float2 z) { return fabsf(z.x) + fabsf(z.y); }
@@ -370,19 +264,6 @@ hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr
     if (n <= 0) return hipSuccess;
     if (general) hipLaunchKernelGGL(k_block0<true>, dim3(n), dim3(64), 0, st, (const float2 *)iq, fr, n, T, corr);
     else hipLaunchKernelGGL(k_block0<false>, dim3(n), dim3(64), 0, st, (const float2 *)iq, fr, n, T, corr);
-    return hipGetLastError();
-}
-hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
-                        const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general) {
-    if (n <= 0) return hipSuccess;
-    const int items = n * nchunks;
-    const dim3 grid((items + DEMOD_WG - 1) / DEMOD_WG), block(64 * DEMOD_WG);
-    if (general)
-        hipLaunchKernelGGL(k_demod<true>, grid, block, 0, st, (const float2 *)iq, fr, items, nchunks, T, soft,
-                           softf, (float2 *)fcpart);
-    else
-        hipLaunchKernelGGL(k_demod<false>, grid, block, 0, st, (const float2 *)iq, fr, items, nchunks, T, soft,
-                           softf, (float2 *)fcpart);
     return hipGetLastError();
 }
 hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
