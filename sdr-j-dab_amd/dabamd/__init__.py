@@ -135,6 +135,13 @@ class DevBuf:
         _chk(lib().dabgpu_memcpy_h2d(self.ctx.h, self.ptr, _p(a), a.nbytes), "h2d")
         return self
 
+    def upload_at(self, a: np.ndarray, offset: int) -> "DevBuf":
+        """copy `a` to byte `offset` of the buffer"""
+        a = np.ascontiguousarray(a)
+        assert offset >= 0 and offset + a.nbytes <= self.nbytes
+        _chk(lib().dabgpu_memcpy_h2d(self.ctx.h, C.c_void_p(self.ptr.value + offset), _p(a), a.nbytes), "h2d")
+        return self
+
     def download(self, dtype, shape) -> np.ndarray:
         out = np.empty(shape, dtype=dtype)
         assert out.nbytes <= self.nbytes

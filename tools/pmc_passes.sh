@@ -5,6 +5,7 @@
 out=$1; shift
 cd /tmp && export TMPDIR=/tmp
 root=${GRAFT_REPO_ROOT:-/root/repo}
+mkdir -p $root/gpurun_out/$out
 i=0
 for ctrs in "$@"; do
     i=$((i+1))
