@@ -98,7 +98,7 @@ struct VitJob {
 
 // DAB+ superframe layer (k_dabplus.hip)
 constexpr int DP_MAX_RS = 48;       // RSDims = bitRate / 8, bitRate <= 384
-constexpr int DP_TAB_BYTES = 256 + 256 + 512 + 2560 + 512;   // GF exp/log, fire, mul[10], crc
+constexpr int DP_TAB_BYTES = 256 + 256 + 512 + 2560 + 512 + 2048;   // GF exp/log, fire, mul[10], crc, pow8
 struct DpState {
     int32_t fill, blocks;           // blockFillIndex, blocksInBuffer (mp4processor.cpp:86-87)
 };
@@ -110,6 +110,7 @@ struct DpJob {
     const int16_t *dp_br;           // [ndp] its bitRate
     uint8_t *ring;                  // [S][ndp][120*DP_MAX_RS] 5-CIF byte rings
     DpState *state;                 // [S][ndp]
+    uint8_t *code;                  // [S][ndp][ncif] scratch: 0 fire code failed, 2 rejected, 3 decoded
     uint8_t *sf_out;                // [S][ncif][ndp][sf_stride]
     int64_t sf_stride;
     dabgpu_superframe *info;        // [S][ncif][ndp]
@@ -128,7 +129,9 @@ hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, i
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
 hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
-hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
+// persist_waves > 0: a persistent launch of that many waves drawing pairs from *ctr
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic, int persist_waves = 0,
+                              int *ctr = nullptr);
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <cstdarg>
 #include <string>
@@ -175,6 +176,11 @@ struct HostTables {
             for (int k = 0; k < 8; k++) c = (c & 0x8000u) ? ((c << 1) ^ 0x1021u) : (c << 1);
             crc[b] = (uint16_t)(c & 0xFFFFu);
         }
+        // x^(8d) mod the CRC polynomial: shifts a partial CRC past d bytes
+        uint16_t *pow8 = (uint16_t *)(dptab.data() + 1024 + 2560 + 512);
+        pow8[0] = 1;
+        for (int d = 1; d < 1024; d++)
+            pow8[d] = (uint16_t)(((uint32_t)pow8[d - 1] << 8) ^ crc[pow8[d - 1] >> 8]);
     }
     std::vector<uint8_t> dptab;             // GF exp[256], log[256], fire uint16[256]
 };
@@ -450,7 +456,9 @@ int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n,
 // rounds * (symbols per chunk + 1 warm-up symbol).
 static const int kMaxChunks = 25;
 static const int kDemodWgPerCu = 3;
-static int demod_chunks(int n) {
+// the persistent ACS keeps this many waves per SIMD (of the 8 its 62 VGPRs allow)
+static const int kAcsWavesPerSimd = 0;
+static int num_cus() {
     static int cus = 0;
     if (!cus) {
         int dev = 0;
@@ -458,6 +466,10 @@ static int demod_chunks(int n) {
             cus = 256;
         cus = std::max(cus, 1);
     }
+    return cus;
+}
+static int demod_chunks(int n) {
+    const int cus = num_cus();
     const int64_t slots = (int64_t)kDemodWgPerCu * cus;
     int best = 1;
     double best_cost = 1e30;
@@ -652,6 +664,8 @@ struct dabgpu_pipe {
     float *fc_d = nullptr, *fcpart_d = nullptr;
     int32_t *slots_d = nullptr;
     uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
+    int *acs_ctr_d = nullptr;                   // [2] pair counters of the persistent ACS
+    int acs_persist = 0;                        // its waves (0: one wave per pair)
     size_t dec_sz = 0;
     int64_t dec_fic_off = 0;                    // FIC decisions: words after the MSC's
     int max_nbits = 0;
@@ -663,6 +677,7 @@ struct dabgpu_pipe {
     int16_t *dp_br_d = nullptr;
     uint8_t *dp_ring_d = nullptr;     // [S][NDP][120*DP_MAX_RS]
     DpState *dp_state_d = nullptr;    // [S][NDP]
+    uint8_t *dp_code_d = nullptr;     // [S][NDP][4F] superframe verdict per candidate CIF
     const uint8_t *last_msc = nullptr; // MSC bits of the last successful run
     int32_t last_msc_stride = 0;
     int64_t last_cif0 = 0;
@@ -773,6 +788,13 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->dec_d[0], p->dec_sz);
     A((void **)&p->dec_d[1], p->dec_sz);
     A((void **)&p->ficprof_d, sizeof(Profile));
+    A((void **)&p->acs_ctr_d, 2 * sizeof(int));
+    {
+        // persistent ACS waves per SIMD (DABGPU_ACS_WPS, 0 = one wave per codeword pair)
+        int wps = kAcsWavesPerSimd;
+        if (const char *e = getenv("DABGPU_ACS_WPS")) wps = std::max(0, std::min(8, atoi(e)));
+        p->acs_persist = wps * 4 * num_cus();
+    }
     int prio_least = 0, prio_greatest = 0;
     if (!rc && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) rc = fail(DABGPU_E_HIP, "priority range");
     if (!rc && (hipStreamCreateWithPriority(&p->vs[0], hipStreamNonBlocking, prio_least) != hipSuccess ||
@@ -807,6 +829,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
         A((void **)&p->dp_br_d, sizeof(int16_t) * dpb.size());
         A((void **)&p->dp_ring_d, (size_t)p->S * p->NDP * 120 * DP_MAX_RS);
         A((void **)&p->dp_state_d, sizeof(DpState) * (size_t)p->S * p->NDP);
+        A((void **)&p->dp_code_d, (size_t)p->S * p->NDP * 4 * p->F);
         if (!rc && (hipMemcpy(p->dp_sub_d, dps.data(), sizeof(int32_t) * dps.size(), hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemcpy(p->dp_br_d, dpb.data(), sizeof(int16_t) * dpb.size(), hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemset(p->dp_ring_d, 0, (size_t)p->S * p->NDP * 120 * DP_MAX_RS) != hipSuccess ||
@@ -838,7 +861,7 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
-                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d})
+                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d, (void *)p->acs_ctr_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
@@ -1175,7 +1198,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     }
     if (fic_bits && do_msc) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs_msc_fic(bs, JM, JF));
+        HIPCHK(launch_acs_msc_fic(bs, JM, JF, p->acs_persist, p->acs_ctr_d + par));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
         HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
@@ -1263,6 +1286,7 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.dp_br = p->dp_br_d;
     J.ring = p->dp_ring_d;
     J.state = p->dp_state_d;
+    J.code = p->dp_code_d;
     J.sf_out = sf_bytes;
     J.sf_stride = sf_stride;
     J.info = info;

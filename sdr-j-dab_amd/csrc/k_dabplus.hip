@@ -2,15 +2,17 @@
 // processSuperframe (mp4processor.cpp:107-292) for every DAB+ subchannel of every
 // stream, over the CIFs one pipeline run decoded.
 //
-// One wave per (stream, DAB+ subchannel) walks that subchannel's CIFs in order:
-// packs the 24*bitRate decoded bits into the 5-CIF byte ring (kept in HBM between
-// runs, in LDS while the wave works), runs the fire-code check at the oldest block
-// (firecode-checker.cpp:76-94) and, when it passes, the RS(120,110) decode of the
-// RSDims interleaved codewords -- one codeword per lane, GF(2^8) tables in LDS --
-// followed by the AU table and the AU CRCs (one AU per lane).  The RS decoder is a
-// restatement of the reference's Karn-style decoder (reed-solomon.cpp:143-399:
-// syndromes, Berlekamp-Massey, Chien search over all 255 positions, Forney), so its
-// return value (errors corrected, or -1) and corrections match it exactly.
+// Two kernels per run.  k_dp_superframe evaluates every superframe candidate of
+// the run in parallel -- one wave per (stream, subchannel, CIF): the fire code at
+// the oldest of the 5 blocks ending at that CIF and, where it holds, the RS(120,110)
+// decode of the RSDims interleaved codewords, the AU table and the AU CRCs.
+// k_dp_walk then runs the reference's sequential block counting (blocksInBuffer)
+// over the candidates' verdicts, which decides which of them the reference would
+// have evaluated, and carries the last 4 CIFs and the state to the next run.  The
+// RS decoder is a restatement of the reference's Karn-style decoder
+// (reed-solomon.cpp:143-399: syndromes, Berlekamp-Massey, Chien search over all 255
+// positions, Forney), so its return value (errors corrected, or -1) and
+// corrections match it exactly.
 #include "dab_device.h"
 #include "dab_kernels.h"
 
@@ -26,6 +28,7 @@ struct GfTabs {
     uint16_t fire[256];      // fire-code syndrome table
     uint8_t mul[10][256];    // s * alpha^i: one lookup per Horner step of syndrome i
     uint16_t crc[256];       // CRC-CCITT (0x1021, msb first) byte table
+    uint16_t pow8[1024];     // x^(8d) mod the CRC polynomial
 };
 static_assert(sizeof(GfTabs) == DP_TAB_BYTES, "host table layout");
 
@@ -174,163 +177,263 @@ __device__ bool fire_ok(const uint8_t *x, const GfTabs &g) {
     return st == 0;
 }
 
-// dabPlus_crc (mp4processor.cpp:40-61)
-__device__ bool au_crc_ok(const uint8_t *msg, int len, int limit, const GfTabs &g) {
-    uint32_t acc = 0xFFFF;
-    const int n = len < limit ? len : limit;
-    for (int i = 0; i < n; i++) acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ msg[i]) & 0xFFu]) & 0xFFFFu;
-    for (int i = n; i < len; i++) acc = ((acc << 8) ^ g.crc[(acc >> 8) & 0xFFu]) & 0xFFFFu;
-    const uint32_t hi = len < limit ? msg[len] : 0, lo = len + 1 < limit ? msg[len + 1] : 0;
-    const uint32_t crc = ~((hi << 8) | lo) & 0xFFFFu;
-    return (crc ^ acc) == 0;
-}
-
 __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__global__ __launch_bounds__(64) void k_dabplus(DpJob J) {
+// byte i of one CIF's decoded bits, 8 bits msb first (addtoFrame, mp4processor.cpp:115-121)
+__device__ __forceinline__ uint32_t pack_byte(const uint8_t *bits, int i) {
+    const uint2 w = *(const uint2 *)(bits + 8 * i);
+    uint32_t t = 0;
+#pragma unroll
+    for (int j = 0; j < 4; j++) t = (t << 1) | ((w.x >> (8 * j)) & 1u);
+#pragma unroll
+    for (int j = 0; j < 4; j++) t = (t << 1) | ((w.y >> (8 * j)) & 1u);
+    return t;
+}
+
+// Byte p of the superframe candidate ending at CIF cl of this run: the 5 blocks
+// cl-4..cl in delivery order, i.e. the reference's ring read from its oldest block
+// (mp4processor.cpp:128-140).  Blocks before the run come from the carry (the
+// previous run's last 4 CIFs, oldest first).
+__device__ __forceinline__ uint32_t window_byte(const DpJob &J, const uint8_t *carry, int stream, int sub,
+                                                int nbytes, int cl, int p) {
+    const int b = p / nbytes, w = p - b * nbytes, q = cl - 4 + b;
+    if (q < 0) return carry[(q + 4) * nbytes + w];
+    return pack_byte(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride, w);
+}
+
+// a * b in GF(2)[x] / (x^16 + x^12 + x^5 + 1)
+__device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
+    uint32_t r = 0;
+#pragma unroll
+    for (int k = 15; k >= 0; k--) {
+        r = ((r << 1) ^ ((r & 0x8000u) ? 0x1021u : 0u)) & 0xFFFFu;
+        if ((b >> k) & 1u) r ^= a;
+    }
+    return r;
+}
+
+__device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v ^= (uint32_t)__shfl_xor((int)v, o, 64);
+    return v;
+}
+
+// Superframe candidates, one wave per (stream, DAB+ subchannel, CIF of the run):
+// the fire code at the oldest block of the 5-CIF window ending at that CIF
+// (firecode-checker.cpp:76-94) and, where it holds, processSuperframe
+// (mp4processor.cpp:146-292): RS(120,110) over the RSDims interleaved columns, AU
+// table, AU CRCs.  Which candidates the reference actually evaluates depends on
+// the superframe state (blocksInBuffer), walked afterwards by k_dp_walk; the
+// verdict of every candidate (0 fire code failed, 2 rejected, 3 decoded) goes to
+// J.code, the record and the corrected bytes of a passing one to their slots.
+// The work of one superframe is spread over the wave: syndromes as direct sums
+// (lane = column x a slice of its rows), Berlekamp-Massey/Chien/Forney one column
+// per lane, each AU CRC in 64 slices joined by x^(8d) shifts (the CRC is linear).
+__global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     __shared__ GfTabs g;
-    __shared__ uint8_t ring[120 * DP_MAX_RS];
-    __shared__ uint8_t outv[110 * DP_MAX_RS + 16];
-    __shared__ int16_t syn_s[10 * DP_MAX_RS];
+    __shared__ uint8_t sfb[120 * DP_MAX_RS];
+    __shared__ uint32_t syn_s[10 * DP_MAX_RS];
     __shared__ uint8_t rl[64 * 40];
     __shared__ int32_t red[64];
     const int lane = threadIdx.x;
-    const int stream = blockIdx.x / J.ndp, dp = blockIdx.x % J.ndp;
+    const int cl = blockIdx.x % J.ncif, sd = blockIdx.x / J.ncif;       // sd = stream * ndp + dp
+    const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
     const int br = J.dp_br[dp], sub = J.dp_sub[dp];
-    const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS;
-    // tables + this subchannel's ring into LDS
-    for (int i = lane; i < (int)sizeof(GfTabs); i += 64) ((uint8_t *)&g)[i] = J.tabs[i];
-    uint8_t *gring = J.ring + ((int64_t)stream * J.ndp + dp) * (120 * DP_MAX_RS);
-    for (int i = lane; i < fsz; i += 64) ring[i] = gring[i];
-    DpState st = J.state[(int64_t)stream * J.ndp + dp];
+    const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
+    uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
+    // a window holding an undelivered CIF (de-interleaver warm-up) is never evaluated
+    if (J.cif0 + cl - 4 < 16) {
+        if (lane == 0) *code = 0;
+        return;
+    }
+    const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
+    const uint32_t *tabs32 = (const uint32_t *)J.tabs;
+    const int fire0 = offsetof(GfTabs, fire) / 4, fire1 = fire0 + (int)sizeof(g.fire) / 4;
+    for (int i = fire0 + lane; i < fire1; i += 64) ((uint32_t *)&g)[i] = tabs32[i];
+    if (lane < 11) sfb[lane] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, lane);
     wave_sync();
-    for (int cl = 0; cl < J.ncif; cl++) {
-        const int64_t rec = ((int64_t)stream * J.ncif + cl) * J.ndp + dp;
-        dabgpu_superframe info;
-        info.status = -1;
-        info.num_aus = 0;
-        info.n_corrected = 0;
-        for (int i = 0; i < 7; i++) info.au_start[i] = 0;
-        info.au_crc_ok = 0;
-        info.reserved = 0;
-        if (J.cif0 + cl < 16) {                          // de-interleaver warm-up: nothing delivered
-            if (lane == 0) J.info[rec] = info;
-            continue;
-        }
-        // addtoFrame: pack 8 bits per byte, msb first, into block `fill` (:115-121)
-        const uint8_t *bits = J.msc + (((int64_t)stream * J.ncif + cl) * J.nsub + sub) * J.msc_stride;
-        for (int i = lane; i < nbytes; i += 64) {
-            const uint2 w = *(const uint2 *)(bits + 8 * i);
-            const uint64_t v = ((uint64_t)w.y << 32) | w.x;
-            uint32_t t = 0;
+    if (!fire_ok(sfb, g)) {
+        if (lane == 0) *code = 0;
+        return;
+    }
+    for (int i = lane; i < DP_TAB_BYTES / 4; i += 64)
+        if (i < fire0 || i >= fire1) ((uint32_t *)&g)[i] = tabs32[i];
+    for (int p = 11 + lane; p < fsz; p += 64) sfb[p] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, p);
+    for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;
+    wave_sync();
+    // syndromes S_i = sum_m r_m alpha^(i (119-m)) per column: the Horner sums of
+    // reed-solomon.cpp:231-266 (roots alpha^0..alpha^9, the 135 zero pad bytes
+    // contribute nothing).  Lane -> column lane % RS, rows lane / RS + k * (64 / RS).
+    const int per = 64 / RS;
+    if (lane < per * RS) {
+        const int j = lane % RS;
+        uint32_t acc[10];
 #pragma unroll
-            for (int j = 0; j < 8; j++) t = (t << 1) | (uint32_t)((v >> (8 * j)) & 1u);
-            ring[st.fill * nbytes + i] = (uint8_t)t;
-        }
-        wave_sync();
-        st.blocks++;
-        st.fill = (st.fill + 1) % 5;
-        info.status = 0;
-        if (st.blocks >= 5) {
-            const int base = st.fill * nbytes;
-            if (!fire_ok(ring + base, g)) {
-                info.status = 1;
-                st.blocks = 4;
-            } else {
-                // processSuperframe: RS over the RSDims interleaved columns (:165-179).
-                // Byte k of column j is ring[(base + j + k*RS) % fsz], so the
-                // uncorrected output outv[j + k*RS] is the ring rotated by base.
-                for (int i = lane; i < 110 * RS; i += 64) {
-                    const int o = base + i;
-                    outv[i] = ring[o < fsz ? o : o - fsz];
-                }
-                // syndromes: every (column, root) pair is one Horner chain on one lane
-                for (int p = lane; p < 10 * RS; p += 64) {
-                    const int j = p / 10, i = p - 10 * j;
-                    syn_s[p] = (int16_t)rs_syndrome(ring, RS, fsz, base + j < fsz ? base + j : base + j - fsz, i, g);
-                }
-                wave_sync();
-                int ler = 0;
-                if (lane < RS) {                                 // one column per lane
-                    int sy[10];
+        for (int i = 0; i < 10; i++) acc[i] = 0;
+        for (int m = lane / RS; m < 120; m += per) {
+            const int r = sfb[j + m * RS];
+            if (r) {
+                const int t = 119 - m;
+                int e = g.log[r];
+                acc[0] ^= g.exp[e];
 #pragma unroll
-                    for (int i = 0; i < 10; i++) sy[i] = syn_s[10 * lane + i];
-                    uint8_t *w = rl + lane * 40;
-                    int nf = 0;
-                    ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
-                    for (int f = 0; f < nf; f++) {
-                        const int m = w[20 + f] - RS_PAD;
-                        if (m >= 0 && m < 110) outv[lane + m * RS] ^= w[30 + f];
-                    }
+                for (int i = 1; i < 10; i++) {
+                    e += t;
+                    if (e >= RS_NN) e -= RS_NN;
+                    acc[i] ^= g.exp[e];
                 }
-                red[lane] = ler;
-                wave_sync();
-                // the reference stops at the first failing column
-                int nerr = 0, fail = 0;
-                for (int j = 0; j < RS && !fail; j++) {
-                    const int l = red[j];
-                    if (l > 0) nerr += l;
-                    if (l < 0) fail = 1;
-                }
-                info.n_corrected = (int16_t)nerr;
-                bool ok = !fail;
-                if (ok) {
-                    // AU table (:181-233)
-                    const int dac = (outv[2] >> 6) & 1, sbr = (outv[2] >> 5) & 1;
-                    int n, a[7];
-                    const int end = 110 * RS;
-                    switch (2 * dac + sbr) {
-                    default:
-                    case 0: n = 4; a[0] = 8; a[1] = outv[3] * 16 + (outv[4] >> 4);
-                        a[2] = (outv[4] & 0xf) * 256 + outv[5]; a[3] = outv[6] * 16 + (outv[7] >> 4); a[4] = end; break;
-                    case 1: n = 2; a[0] = 5; a[1] = outv[3] * 16 + (outv[4] >> 4); a[2] = end; break;
-                    case 2: n = 6; a[0] = 11; a[1] = outv[3] * 16 + (outv[4] >> 4);
-                        a[2] = (outv[4] & 0xf) * 256 + outv[5]; a[3] = outv[6] * 16 + (outv[7] >> 4);
-                        a[4] = (outv[7] & 0xf) * 256 + outv[8]; a[5] = outv[9] * 16 + (outv[10] >> 4); a[6] = end; break;
-                    case 3: n = 3; a[0] = 6; a[1] = outv[3] * 16 + (outv[4] >> 4);
-                        a[2] = (outv[4] & 0xf) * 256 + outv[5]; a[3] = end; break;
-                    }
-                    info.num_aus = (int8_t)n;
-                    for (int i = 0; i < 7; i++) info.au_start[i] = (int16_t)(i <= n ? a[i] : 0);
-                    int bad = n;                                  // first AU with an impossible layout
-                    for (int i = 0; i < n; i++) {
-                        const int len = a[i + 1] - a[i] - 2;
-                        if (a[i + 1] < a[i] || len >= 960 || len < 0) { bad = i; break; }
-                    }
-                    // one AU per lane: CRC over [a[i], a[i+1])
-                    int mine = 0;
-                    if (lane < bad) {
-                        int ai = 0, an = 0;
-                        for (int i = 0; i < 7; i++) if (i == lane) { ai = a[i]; an = a[i + 1]; }
-                        const int len = an - ai - 2;
-                        mine = au_crc_ok(outv + ai, len, end - ai, g) ? 1 : 0;
-                    }
-                    const uint64_t crcmask = __ballot(mine);
-                    info.au_crc_ok = (uint8_t)(crcmask & 0x3F);
-                    ok = bad == n;
-                }
-                info.status = ok ? 3 : 2;
-                st.blocks = ok ? 0 : 4;
-                if (ok) {
-                    uint8_t *o = J.sf_out + rec * J.sf_stride;
-                    for (int i = lane; i < 110 * RS; i += 64) o[i] = outv[i];
-                }
-                wave_sync();
             }
         }
-        if (lane == 0) J.info[rec] = info;
+#pragma unroll
+        for (int i = 0; i < 10; i++)
+            if (acc[i]) atomicXor(&syn_s[10 * j + i], acc[i]);
     }
-    for (int i = lane; i < fsz; i += 64) gring[i] = ring[i];
-    if (lane == 0) J.state[(int64_t)stream * J.ndp + dp] = st;
+    wave_sync();
+    int ler = 0;
+    if (lane < RS) {                                     // one column per lane
+        int sy[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) sy[i] = (int)syn_s[10 * lane + i];
+        uint8_t *w = rl + lane * 40;
+        int nf = 0;
+        ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
+        for (int f = 0; f < nf; f++) {
+            const int m = w[20 + f] - RS_PAD;
+            if (m >= 0 && m < 110) sfb[lane + m * RS] ^= w[30 + f];
+        }
+    }
+    red[lane] = ler;
+    wave_sync();
+    // the reference stops at the first failing column
+    int nerr = 0, fail = 0;
+    for (int j = 0; j < RS && !fail; j++) {
+        const int l = red[j];
+        if (l > 0) nerr += l;
+        if (l < 0) fail = 1;
+    }
+    dabgpu_superframe info;
+    info.status = 2;
+    info.num_aus = 0;
+    info.n_corrected = (int16_t)nerr;
+    for (int i = 0; i < 7; i++) info.au_start[i] = 0;
+    info.au_crc_ok = 0;
+    info.reserved = 0;
+    bool ok = !fail;
+    if (ok) {
+        // AU table (:181-233)
+        const int dac = (sfb[2] >> 6) & 1, sbr = (sfb[2] >> 5) & 1;
+        int n, a[7];
+        switch (2 * dac + sbr) {
+        default:
+        case 0: n = 4; a[0] = 8; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4); a[4] = end; break;
+        case 1: n = 2; a[0] = 5; a[1] = sfb[3] * 16 + (sfb[4] >> 4); a[2] = end; break;
+        case 2: n = 6; a[0] = 11; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4);
+            a[4] = (sfb[7] & 0xf) * 256 + sfb[8]; a[5] = sfb[9] * 16 + (sfb[10] >> 4); a[6] = end; break;
+        case 3: n = 3; a[0] = 6; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = end; break;
+        }
+        info.num_aus = (int8_t)n;
+        for (int i = 0; i < 7; i++) info.au_start[i] = (int16_t)(i <= n ? a[i] : 0);
+        int bad = n;                                     // first AU with an impossible layout
+        for (int i = 0; i < n; i++) {
+            const int len = a[i + 1] - a[i] - 2;
+            if (a[i + 1] < a[i] || len >= 960 || len < 0) { bad = i; break; }
+        }
+        // dabPlus_crc (mp4processor.cpp:40-61) of AU i over [a[i], a[i+1]): lane l
+        // runs the table CRC over its slice (lane 0 from the 0xFFFF preset, the others
+        // from 0), shifts it past the bytes after the slice, and the slices XOR
+        // together.  Bytes past the superframe read as zero.
+        uint32_t mask = 0;
+        for (int i = 0; i < bad; i++) {
+            const int ai = a[i], len = a[i + 1] - ai - 2, limit = end - ai;
+            const int cs = (len + 63) >> 6;
+            const int k0 = min(len, lane * cs), k1 = min(len, k0 + cs);
+            uint32_t acc = lane == 0 ? 0xFFFFu : 0u;
+            for (int k = k0; k < k1; k++) {
+                const uint32_t b = k < limit ? sfb[ai + k] : 0u;
+                acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ b) & 0xFFu]) & 0xFFFFu;
+            }
+            if (acc) acc = crc_mulmod(acc, g.pow8[len - k1]);
+            acc = wave_xor(acc);
+            const uint32_t hi = len < limit ? sfb[ai + len] : 0u, lo = len + 1 < limit ? sfb[ai + len + 1] : 0u;
+            if (((~((hi << 8) | lo) & 0xFFFFu) ^ acc) == 0) mask |= 1u << i;
+        }
+        info.au_crc_ok = (uint8_t)(mask & 0x3F);
+        ok = bad == n;
+    }
+    if (ok) {
+        info.status = 3;
+        uint8_t *o = J.sf_out + (((int64_t)stream * J.ncif + cl) * J.ndp + dp) * J.sf_stride;
+        for (int i = lane; i < end; i += 64) o[i] = sfb[i];
+    }
+    if (lane == 0) {
+        J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
+        *code = (uint8_t)info.status;
+    }
+}
+
+// The superframe state machine of addtoFrame (mp4processor.cpp:107-145) over the
+// run's CIFs, one wave per (stream, DAB+ subchannel): blocksInBuffer decides which
+// candidates are evaluated; their verdicts come from k_dp_superframe.  Writes the
+// records of the CIFs without an evaluated superframe, the state, and the carry
+// (the run's last 4 CIFs as bytes) for the next run.
+__global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
+    const int lane = threadIdx.x, sd = blockIdx.x;
+    const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
+    const int br = J.dp_br[dp], sub = J.dp_sub[dp], nbytes = 3 * br;
+    DpState st = J.state[sd];
+    const uint8_t *code = J.code + (int64_t)sd * J.ncif;
+    for (int c0 = 0; c0 < J.ncif; c0 += 64) {
+        const int cl = c0 + lane;
+        const int v = cl < J.ncif ? code[cl] : 0;
+        int fs = 0;
+        const int nc = min(64, J.ncif - c0);
+        for (int i = 0; i < nc; i++) {                  // uniform
+            int s;
+            if (J.cif0 + c0 + i < 16) {
+                s = -1;                                  // de-interleaver warm-up: nothing delivered
+            } else {
+                st.blocks++;
+                st.fill = (st.fill + 1) % 5;
+                s = 0;
+                if (st.blocks >= 5) {
+                    const int cd = __builtin_amdgcn_readlane(v, i);
+                    s = cd == 0 ? 1 : cd;
+                    st.blocks = cd == 3 ? 0 : 4;
+                }
+            }
+            if (lane == i) fs = s;
+        }
+        if (cl < J.ncif && fs < 2) {
+            dabgpu_superframe info;
+            info.status = (int8_t)fs;
+            info.num_aus = 0;
+            info.n_corrected = 0;
+            for (int i = 0; i < 7; i++) info.au_start[i] = 0;
+            info.au_crc_ok = 0;
+            info.reserved = 0;
+            J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
+        }
+    }
+    uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
+    for (int p = lane; p < 4 * nbytes; p += 64) {
+        const int b = p / nbytes, w = p - b * nbytes, q = J.ncif - 4 + b;
+        carry[p] = (uint8_t)pack_byte(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride, w);
+    }
+    if (lane == 0) J.state[sd] = st;
 }
 
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job) {
     if (job.ndp <= 0 || job.nstreams <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_dabplus, dim3(job.nstreams * job.ndp), dim3(64), 0, st, job);
+    if (job.ncif < 4) return hipErrorInvalidValue;       // the carry holds the last 4 CIFs
+    hipLaunchKernelGGL(k_dp_superframe, dim3(job.nstreams * job.ndp * job.ncif), dim3(64), 0, st, job);
+    hipLaunchKernelGGL(k_dp_walk, dim3(job.nstreams * job.ndp), dim3(64), 0, st, job);
     return hipGetLastError();
 }
 

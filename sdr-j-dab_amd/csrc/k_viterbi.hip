@@ -11,30 +11,31 @@
 //               (v_pk_add_u16 / v_pk_min_u16 do both).  Exactness of 16 bits: metric
 //               spread across states is <= 6 * 1020 (every state is reachable from the
 //               best one in 6 steps, branch metrics are in [0, 1020]), so subtracting a
-//               common offset every 48 steps keeps every metric in [0, 61326] and every
+//               common offset every 30 steps keeps every metric in [0, 43860] and every
 //               comparison equal to the reference's uint32 one.
 //               States are relabelled every step (lane L holds state rotl6(L, t mod 6)),
 //               so a butterfly pairs lanes at xor distance 32,16,8,4,2,1.  Each lane
 //               forms its two candidates as (metric of the LOWER lane of its pair) +
 //               row A and (metric of the UPPER lane) + row B, the rows chosen per lane
-//               so that the decision is "cand0 > cand1" in every lane: one compare per
-//               codeword per step.  The broadcasts are DPP (quad_perm, row_shr/shl with
-//               bank masks) or one permlane16/32_swap.  Each lane shifts its decision
-//               bits into a 32-bit word per codeword (v_addc with the compare mask as
-//               carry-in) and stores it every 32 steps: decisions never leave the VGPRs
-//               as scalar masks.  Branch metrics for 96 steps are built in LDS by the
-//               lanes at once (depuncturing + 16-CIF time de-interleave fused into that
-//               gather), both codewords packed per word.
+//               so that the decision is "A > B" in every lane.  The broadcasts are DPP
+//               (quad_perm, row_shr/shl with bank masks) or one permlane16/32_swap.
+//               Both codewords' decisions come from one packed subtract (sign bits of
+//               B - A) and shift into one VGPR (dec_in); every 30 steps they are
+//               unpacked into one 30-bit word per codeword and stored: decisions never
+//               leave the VGPRs as scalar masks.  Branch metrics for 60 steps are built
+//               in LDS by the lanes at once (depuncturing + 16-CIF time de-interleave
+//               fused into that gather), both codewords packed per word.
 //   k_traceback one LANE per codeword, 64 chainbacks per wave in lock-step.  Decision
-//               words of a 32-step chunk for the wave's 64 codewords are staged in LDS
-//               (16 KB, double-buffered against the next chunk's loads); each step reads
-//               the word of the lane that held the traced state.  Bits leave through
-//               4-B stores with the energy-dispersal PRBS xor-ed in.
+//               words of a 30-step chunk for the wave's 64 codewords are staged in LDS
+//               (16 KB, register-prefetched 2 chunks ahead); each step reads the word of
+//               the lane that held the traced state, two steps per LDS round trip.
+//               Bits leave through 2-B stores with the energy-dispersal PRBS xor-ed in.
 //
-// Decision layout: dec[(chunk * dec_ncw + row) * 64 + lane] (uint32), bit (31 - k) =
-// decision of `lane` at trellis step 32*chunk + k.
+// Decision layout: dec[(chunk * dec_ncw + row) * 64 + lane] (uint32), bit k =
+// decision of `lane` at trellis step 30*chunk + k (k < 30).
 #include "dab_device.h"
 #include "dab_kernels.h"
+#include <algorithm>
 
 namespace dab {
 
@@ -261,11 +262,12 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 template <int M>
 __device__ __forceinline__ void bcast(uint32_t x, uint32_t &P, uint32_t &Q) {
     if constexpr (M == 1) {
-        P = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xA0, 0xF, 0xF, false);        // quad_perm [0,0,2,2]
-        Q = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xF5, 0xF, 0xF, false);        // quad_perm [1,1,3,3]
+        // every lane is written: no old value (update_dpp(0, ..) would zero a register first)
+        P = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);        // quad_perm [0,0,2,2]
+        Q = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);        // quad_perm [1,1,3,3]
     } else if constexpr (M == 2) {
-        P = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x44, 0xF, 0xF, false);        // quad_perm [0,1,0,1]
-        Q = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0xEE, 0xF, 0xF, false);        // quad_perm [2,3,2,3]
+        P = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x44, 0xF, 0xF, false);        // quad_perm [0,1,0,1]
+        Q = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xEE, 0xF, 0xF, false);        // quad_perm [2,3,2,3]
     } else if constexpr (M == 4) {
         // upper lanes (banks 1,3 of each row) take lane-4; lower lanes (banks 0,2) lane+4
         Q = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x104, 0xF, 0x5, false);  // row_shl:4
@@ -285,12 +287,11 @@ __device__ __forceinline__ void bcast(uint32_t x, uint32_t &P, uint32_t &Q) {
     }
 }
 
-// acc = 2*acc + (lane's bit of mask): the decision enters as the carry-in
-__device__ __forceinline__ uint32_t shift_in(uint32_t acc, uint64_t mask) {
-    uint32_t r;
-    uint64_t co;
-    asm("v_addc_co_u32_e64 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(acc), "s"(mask));
-    return r;
+// w = (w >> 1) with the sign bits of d (bits 15 and 31) inserted at bits 15 and 31:
+// one decision per codeword per step (one v_lshrrev + one v_bfi)
+__device__ __forceinline__ uint32_t dec_in(uint32_t w, uint32_t d) {
+    const uint32_t M = __builtin_amdgcn_readfirstlane(0x80008000u);   // an SGPR operand of v_bfi
+    return (d & M) | ((w >> 1) & ~M);
 }
 
 // subtract a common offset from all states of each codeword (see header)
@@ -306,10 +307,22 @@ __device__ __forceinline__ uint32_t renorm(uint32_t x) {
 // half of the tile table.  The words are stored at chunk `ch`; rb[k]: word offset of
 // codeword k's chunk 0 in dec (wave-uniform; < 0: not stored).  One copy of this code
 // serves every word (small hot loop: the instruction cache holds it).
+// Decisions: d = B - A per 16-bit half has its sign bit set iff A > B (|A - B| <=
+// spread + 1020 < 2^15), so one packed subtract yields both codewords' decisions;
+// they shift down their half of w (dec_in), 15 steps per half-word, and are
+// unpacked to one word per codeword (step k at bit k) at the end of the word.
 template <int NP, bool FULL>
-__device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP],
-                                         uint32_t (&acc)[2 * NP], int nst, uint32_t *dec,
-                                         const int64_t (&rb)[2 * NP], int64_t o, int lane) {
+__device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
+                                         uint32_t *dec, const int64_t (&rb)[2 * NP], int64_t o, int lane) {
+    static_assert(WS == 30, "two 15-step half-words per decision word");
+    // the 6 per-phase row addresses once per word: each step's read is then one
+    // ds_read_b64 at an immediate offset
+    const uint32_t *rp[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) rp[r] = bm + row[r];
+    uint32_t w[NP], w0[NP];
+#pragma unroll
+    for (int p = 0; p < NP; p++) w[p] = 0;
     sfor<0, WS>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         constexpr int rho = j % 6;
@@ -318,18 +331,28 @@ __device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&ro
                 constexpr int p = decltype(pc)::value;
                 uint32_t P, Q;
                 bcast<(32 >> rho)>(x[p], P, Q);
-                const uint2 t = *(const uint2 *)(bm + p * 8 * BRS + row[rho] + 2 * j);
+                const uint2 t = *(const uint2 *)(rp[rho] + p * 8 * BRS + 2 * j);
                 const u16x2 A = as_pk(P) + as_pk(t.x), B = as_pk(Q) + as_pk(t.y);
-                acc[2 * p] = shift_in(acc[2 * p], __builtin_amdgcn_ballot_w64(A.x > B.x));
-                acc[2 * p + 1] = shift_in(acc[2 * p + 1], __builtin_amdgcn_ballot_w64(A.y > B.y));
+                w[p] = dec_in(w[p], as_u32(B - A));
                 x[p] = as_u32(__builtin_elementwise_min(A, B));
             });
+        } else {
+#pragma unroll
+            for (int p = 0; p < NP; p++) w[p] = dec_in(w[p], 0u);   // keep the bit positions
+        }
+        if constexpr (j == WS / 2 - 1) {
+#pragma unroll
+            for (int p = 0; p < NP; p++) w0[p] = w[p];
         }
     });
-    const int sh = FULL ? 0 : WS - nst;                  // step k of the word at bit WS-1-k
+    // half-word h holds step 15h + k at bit k + 1 (codeword 0) and k + 17 (codeword 1)
 #pragma unroll
-    for (int k = 0; k < 2 * NP; k++)
-        if (rb[k] >= 0) (dec + rb[k] + o)[lane] = acc[k] << sh;
+    for (int p = 0; p < NP; p++) {
+        const uint32_t c0 = ((w0[p] >> 1) & 0x7FFFu) | ((w[p] << 14) & 0x3FFF8000u);
+        const uint32_t c1 = ((w0[p] >> 17) & 0x7FFFu) | ((w[p] >> 2) & 0x3FFF8000u);
+        if (rb[2 * p] >= 0) (dec + rb[2 * p] + o)[lane] = c0;
+        if (rb[2 * p + 1] >= 0) (dec + rb[2 * p + 1] + o)[lane] = c1;
+    }
 #pragma unroll
     for (int p = 0; p < NP; p++) x[p] = renorm(x[p]);
 }
@@ -373,13 +396,12 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         const bool upper = (lane >> (5 - r)) & 1;
         row[r] = (uint32_t)((upper ? q ^ 7 : q) * BRS);
     }
-    uint32_t x[NP], acc[2 * NP];
+    uint32_t x[NP];
     int64_t rb[2 * NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) x[p] = lane == 0 ? 0u : 0x003F003Fu;   // viterbi.cpp:360-371
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++) {
-        acc[k] = 0;
         rb[k] = c[k].valid ? (int64_t)c[k].row * 64 : -1;
     }
     const int64_t cstride = J.dec_ncw * 64;
@@ -421,8 +443,8 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
             const int tw = t0 + u * WS;
             if (tw >= steps) break;
             const int64_t o = (int64_t)(tw / WS) * cstride;
-            if (tw + WS <= steps) acs_word<NP, true>(bm + 2 * WS * u, row, x, acc, WS, J.dec, rb, o, lane);
-            else acs_word<NP, false>(bm + 2 * WS * u, row, x, acc, steps - tw, J.dec, rb, o, lane);
+            if (tw + WS <= steps) acs_word<NP, true>(bm + 2 * WS * u, row, x, WS, J.dec, rb, o, lane);
+            else acs_word<NP, false>(bm + 2 * WS * u, row, x, steps - tw, J.dec, rb, o, lane);
         }
         wave_sync();
     }
@@ -518,11 +540,11 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
                 const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);   // phase of step t0+k is k % 6
                 const uint32_t b1 = 1u << p1, b2 = 1u << p2;
                 const uint32_t w1 = mine[lr], c0 = mine[lr & ~b1], c1 = mine[lr | b1];
-                const uint32_t m1 = (uint32_t)((int32_t)(w1 << (32 - WS + k)) >> 31); // -(bit WS-1-k)
+                const uint32_t m1 = (uint32_t)((int32_t)(w1 << (31 - k)) >> 31);     // -(bit k)
                 w |= (k >= p1 ? ((uint32_t)lr << (k - p1)) : ((uint32_t)lr >> (p1 - k))) & (1u << k);
                 lr = (int)((m1 & b1) | ((uint32_t)lr & ~b1));
                 const uint32_t w2 = (m1 & c1) | (~m1 & c0);
-                const uint32_t m2 = (uint32_t)((int32_t)(w2 << (32 - WS + k - 1)) >> 31);
+                const uint32_t m2 = (uint32_t)((int32_t)(w2 << (32 - k)) >> 31);
                 w |= ((k - 1) >= p2 ? ((uint32_t)lr << (k - 1 - p2)) : ((uint32_t)lr >> (p2 - k + 1))) & (1u << (k - 1));
                 lr = (int)((m2 & b2) | ((uint32_t)lr & ~b2));
             }
@@ -534,7 +556,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
                 const uint32_t w1 = mine[lr];
                 const uint32_t c0 = mine[lr & ~(1 << p1)], c1 = mine[lr | (1 << p1)];
                 {
-                    const int d = (int)((w1 >> (WS - 1 - k)) & 1u);  // predecessor's msb
+                    const int d = (int)((w1 >> k) & 1u);             // predecessor's msb
                     const int u = (lr >> p1) & 1;                     // decoded bit of step t0 + k
                     const int nl = (lr & ~(1 << p1)) | (d << p1);
                     if (full || t0 + k < steps) {
@@ -544,7 +566,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
                 }
                 {
                     const uint32_t w2 = ((lr >> p1) & 1) ? c1 : c0;   // = mine[lr]
-                    const int d = (int)((w2 >> (WS - k)) & 1u);
+                    const int d = (int)((w2 >> (k - 1)) & 1u);
                     const int u = (lr >> p2) & 1;
                     const int nl = (lr & ~(1 << p2)) | (d << p2);
                     if (full || t0 + k - 1 < steps) {
@@ -585,6 +607,23 @@ __global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
     const int b = blockIdx.x;
     if (b < nwa) acs_body<KA, 1>(A, xcd_order(b, nwa), L);
     else acs_body<KB, 1>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
+}
+// the same as a persistent launch: `gridDim.x` waves (a few per SIMD) draw codeword
+// pairs from a counter, MSC first, so the ACS leaves wave slots (VGPRs, LDS) free on
+// every SIMD for the next run's front end -- HBM-bound demod waves beside the
+// issue-bound ACS instead of after it
+template <int KA, int KB>
+__global__ __launch_bounds__(64, 8) void k_acs2p(VitJob A, VitJob B, int nwa, int ntot, int *ctr) {
+    __shared__ AcsLds<1> L;
+    for (;;) {
+        int b = 0;
+        if (threadIdx.x == 0) b = atomicAdd(ctr, 1);
+        b = __builtin_amdgcn_readfirstlane(b);
+        if (b >= ntot) break;
+        if (b < nwa) acs_body<KA, 1>(A, b, L);
+        else acs_body<KB, 1>(B, b - nwa, L);
+        wave_sync();
+    }
 }
 template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
@@ -647,10 +686,17 @@ hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     return e != hipSuccess ? e : launch_traceback(st, job);
 }
 // MSC (a) and FIC (b) decoded by one ACS launch and one traceback launch
-hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b, int persist_waves, int *ctr) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
     if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw)) return hipErrorInvalidValue;
     const int nwa = (a.n_cw + 1) / 2, nwb = (b.n_cw + 1) / 2;
+    if (persist_waves > 0 && ctr) {
+        hipError_t e = hipMemsetAsync(ctr, 0, sizeof(int), st);
+        if (e != hipSuccess) return e;
+        const int g = std::min(persist_waves, nwa + nwb);
+        hipLaunchKernelGGL((k_acs2p<SRC_MSC, SRC_FIC>), dim3(g), dim3(64), 0, st, a, b, nwa, nwa + nwb, ctr);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
     return hipGetLastError();
 }
