@@ -258,40 +258,52 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
     for (int q = 4; q < 8; q++) *(uint2 *)&bm[q * BRS + 2 * j] = make_uint2(wc[7 - q], w[7 - q]);
 }
 
-// (P, Q) = metric of the lower / upper lane of this lane's butterfly pair (xor M)
+// Candidates of one step: A = P + ta, B = Q + tb with (P, Q) = metric of the lower /
+// upper lane of this lane's butterfly pair (xor M).  The packed halves never carry
+// (<= 42840 + 1020 < 2^16), so 32-bit adds serve both codewords and the lane moves
+// fold into them as DPP operands: quad_perm for M = 1, 2; for M = 4, 8 the own-lane
+// sum first, then a bank-masked DPP add over the lanes that take their partner's
+// metric; M = 16, 32 go through one permlane swap.  (s_nop 1: the DPP source may have
+// been written by the previous VALU instruction.)
+#define DPP_ADD(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
 template <int M>
-__device__ __forceinline__ void bcast(uint32_t x, uint32_t &P, uint32_t &Q) {
+__device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint32_t &A, uint32_t &B) {
     if constexpr (M == 1) {
-        // every lane is written: no old value (update_dpp(0, ..) would zero a register first)
-        P = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xA0, 0xF, 0xF, false);        // quad_perm [0,0,2,2]
-        Q = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xF5, 0xF, 0xF, false);        // quad_perm [1,1,3,3]
+        asm(DPP_ADD("quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
+        asm(DPP_ADD("quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 2) {
-        P = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x44, 0xF, 0xF, false);        // quad_perm [0,1,0,1]
-        Q = (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xEE, 0xF, 0xF, false);        // quad_perm [2,3,2,3]
+        asm(DPP_ADD("quad_perm:[0,1,0,1] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
+        asm(DPP_ADD("quad_perm:[2,3,2,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 4) {
-        // upper lanes (banks 1,3 of each row) take lane-4; lower lanes (banks 0,2) lane+4
-        Q = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x104, 0xF, 0x5, false);  // row_shl:4
-        P = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x114, 0xF, 0xA, false);  // row_shr:4
+        // upper lanes (banks 1,3 of each row) take lane-4 as P; lower lanes (banks 0,2) lane+4 as Q
+        A = x + ta;
+        B = x + tb;
+        asm(DPP_ADD("row_shr:4 row_mask:0xf bank_mask:0xa") : "+v"(A) : "v"(x), "v"(ta));
+        asm(DPP_ADD("row_shl:4 row_mask:0xf bank_mask:0x5") : "+v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 8) {
-        Q = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x108, 0xF, 0x3, false);  // row_shl:8
-        P = (uint32_t)__builtin_amdgcn_update_dpp((int)x, (int)x, 0x118, 0xF, 0xC, false);  // row_shr:8
+        A = x + ta;
+        B = x + tb;
+        asm(DPP_ADD("row_shr:8 row_mask:0xf bank_mask:0xc") : "+v"(A) : "v"(x), "v"(ta));
+        asm(DPP_ADD("row_shl:8 row_mask:0xf bank_mask:0x3") : "+v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 16) {
         auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);   // odd rows <-> even rows
-        P = r[0];
-        Q = r[1];
+        A = r[0] + ta;
+        B = r[1] + tb;
     } else {
         static_assert(M == 32, "xor distance");
         auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
-        P = r[0];
-        Q = r[1];
+        A = r[0] + ta;
+        B = r[1] + tb;
     }
 }
+#undef DPP_ADD
 
 // w = (w >> 1) with the sign bits of d (bits 15 and 31) inserted at bits 15 and 31:
 // one decision per codeword per step (one v_lshrrev + one v_bfi)
 __device__ __forceinline__ uint32_t dec_in(uint32_t w, uint32_t d) {
-    const uint32_t M = __builtin_amdgcn_readfirstlane(0x80008000u);   // an SGPR operand of v_bfi
-    return (d & M) | ((w >> 1) & ~M);
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x80008000u), "v"(d), "v"(w >> 1));
+    return r;
 }
 
 // subtract a common offset from all states of each codeword (see header)
@@ -329,12 +341,11 @@ __device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&ro
         if (FULL || j < nst) {
             sfor<0, NP>([&](auto pc) {
                 constexpr int p = decltype(pc)::value;
-                uint32_t P, Q;
-                bcast<(32 >> rho)>(x[p], P, Q);
                 const uint2 t = *(const uint2 *)(rp[rho] + p * 8 * BRS + 2 * j);
-                const u16x2 A = as_pk(P) + as_pk(t.x), B = as_pk(Q) + as_pk(t.y);
-                w[p] = dec_in(w[p], as_u32(B - A));
-                x[p] = as_u32(__builtin_elementwise_min(A, B));
+                uint32_t A, B;
+                cand<(32 >> rho)>(x[p], t.x, t.y, A, B);
+                w[p] = dec_in(w[p], as_u32(as_pk(B) - as_pk(A)));
+                x[p] = as_u32(__builtin_elementwise_min(as_pk(A), as_pk(B)));
             });
         } else {
 #pragma unroll
