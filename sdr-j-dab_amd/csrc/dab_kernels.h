@@ -129,9 +129,7 @@ hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, i
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
 hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
-// persist_waves > 0: a persistent launch of that many waves drawing pairs from *ctr
-hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic, int persist_waves = 0,
-                              int *ctr = nullptr);
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);

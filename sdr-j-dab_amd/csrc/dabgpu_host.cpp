@@ -456,8 +456,6 @@ int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n,
 // rounds * (symbols per chunk + 1 warm-up symbol).
 static const int kMaxChunks = 25;
 static const int kDemodWgPerCu = 3;
-// the persistent ACS keeps this many waves per SIMD (of the 8 its 62 VGPRs allow)
-static const int kAcsWavesPerSimd = 0;
 static int num_cus() {
     static int cus = 0;
     if (!cus) {
@@ -664,8 +662,6 @@ struct dabgpu_pipe {
     float *fc_d = nullptr, *fcpart_d = nullptr;
     int32_t *slots_d = nullptr;
     uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
-    int *acs_ctr_d = nullptr;                   // [2] pair counters of the persistent ACS
-    int acs_persist = 0;                        // its waves (0: one wave per pair)
     size_t dec_sz = 0;
     int64_t dec_fic_off = 0;                    // FIC decisions: words after the MSC's
     int max_nbits = 0;
@@ -788,13 +784,6 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->dec_d[0], p->dec_sz);
     A((void **)&p->dec_d[1], p->dec_sz);
     A((void **)&p->ficprof_d, sizeof(Profile));
-    A((void **)&p->acs_ctr_d, 2 * sizeof(int));
-    {
-        // persistent ACS waves per SIMD (DABGPU_ACS_WPS, 0 = one wave per codeword pair)
-        int wps = kAcsWavesPerSimd;
-        if (const char *e = getenv("DABGPU_ACS_WPS")) wps = std::max(0, std::min(8, atoi(e)));
-        p->acs_persist = wps * 4 * num_cus();
-    }
     int prio_least = 0, prio_greatest = 0;
     if (!rc && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) rc = fail(DABGPU_E_HIP, "priority range");
     if (!rc && (hipStreamCreateWithPriority(&p->vs[0], hipStreamNonBlocking, prio_least) != hipSuccess ||
@@ -861,7 +850,7 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
-                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d, (void *)p->acs_ctr_d})
+                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
@@ -1198,7 +1187,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     }
     if (fic_bits && do_msc) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs_msc_fic(bs, JM, JF, p->acs_persist, p->acs_ctr_d + par));
+        HIPCHK(launch_acs_msc_fic(bs, JM, JF));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
         HIPCHK(launch_traceback_msc_fic(bs, JM, JF));

@@ -619,23 +619,6 @@ __global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
     if (b < nwa) acs_body<KA, 1>(A, xcd_order(b, nwa), L);
     else acs_body<KB, 1>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
 }
-// the same as a persistent launch: `gridDim.x` waves (a few per SIMD) draw codeword
-// pairs from a counter, MSC first, so the ACS leaves wave slots (VGPRs, LDS) free on
-// every SIMD for the next run's front end -- HBM-bound demod waves beside the
-// issue-bound ACS instead of after it
-template <int KA, int KB>
-__global__ __launch_bounds__(64, 8) void k_acs2p(VitJob A, VitJob B, int nwa, int ntot, int *ctr) {
-    __shared__ AcsLds<1> L;
-    for (;;) {
-        int b = 0;
-        if (threadIdx.x == 0) b = atomicAdd(ctr, 1);
-        b = __builtin_amdgcn_readfirstlane(b);
-        if (b >= ntot) break;
-        if (b < nwa) acs_body<KA, 1>(A, b, L);
-        else acs_body<KB, 1>(B, b - nwa, L);
-        wave_sync();
-    }
-}
 template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     __shared__ uint32_t stage[2][TB_WORDS];
@@ -681,7 +664,7 @@ template <int KIND> struct TbK { static auto fn() { return k_traceback<KIND>; } 
 // One codeword pair per wave (NP = 1).  NP > 1 (independent chains interleaved in one
 // wave, fewer waves) measured slower on MI355X for the C3 batch: 0.81 ms (NP=2) and
 // 1.14 ms (NP=3) vs 0.72 ms per launch -- thread-level parallelism hides the
-// compare -> carry and DPP hazards better than instruction-level parallelism here.
+// DPP hazards and LDS latency better than instruction-level parallelism here.
 hipError_t launch_acs(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
     if (job.dec_ncw < dec_rows(job.n_cw)) return hipErrorInvalidValue;
@@ -697,17 +680,10 @@ hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     return e != hipSuccess ? e : launch_traceback(st, job);
 }
 // MSC (a) and FIC (b) decoded by one ACS launch and one traceback launch
-hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b, int persist_waves, int *ctr) {
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
     if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw)) return hipErrorInvalidValue;
     const int nwa = (a.n_cw + 1) / 2, nwb = (b.n_cw + 1) / 2;
-    if (persist_waves > 0 && ctr) {
-        hipError_t e = hipMemsetAsync(ctr, 0, sizeof(int), st);
-        if (e != hipSuccess) return e;
-        const int g = std::min(persist_waves, nwa + nwb);
-        hipLaunchKernelGGL((k_acs2p<SRC_MSC, SRC_FIC>), dim3(g), dim3(64), 0, st, a, b, nwa, nwa + nwb, ctr);
-        return hipGetLastError();
-    }
     hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
     return hipGetLastError();
 }
