@@ -470,7 +470,9 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 // lr, common when the streams carry similar data) read 64 different banks
 constexpr int TB_ROW = 65;
 constexpr int TB_WORDS = 64 * TB_ROW;      // one chunk of a wave's 64 codewords
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // (HIP's uint4 copies as a memcpy -> scratch)
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+constexpr int TB_GROUP = 8;                 // chunks per output flush (240 bits per codeword)
+constexpr int TB_PRBS = 1024;              // PRBS words (fic-handler.cpp:100-108: 32768 bits)
 __device__ __forceinline__ void tb_load(u32x4 (&r)[16], const uint32_t *blk, int lane) {
     const u32x4 *q = (const u32x4 *)blk;
 #pragma unroll
@@ -490,7 +492,7 @@ __device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[16], in
 }
 
 template <int KIND>
-__device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*stage)[TB_WORDS]) {
+__device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*stage)[TB_WORDS], uint32_t *prbs_l) {
     // a latency-bound chain that issues little: first pick on its SIMD, so it keeps
     // its pace next to throughput-bound waves of other kernels (the next run's demod)
     __builtin_amdgcn_s_setprio(3);
@@ -520,6 +522,13 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     smin = __builtin_amdgcn_readfirstlane(smin);
     uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
     const int nch = (tmax + WS - 1) / WS;
+    // the energy-dispersal words in LDS: a vector load of them beside the decision
+    // prefetches would wait for every outstanding load (vmcnt(0)) once per chunk
+    if (J.prbs) {
+        const int nw = min(TB_PRBS, (tmax + WS) / 32 + 2);
+        for (int i = lane; i < nw; i += 64) prbs_l[i] = J.prbs_words[i];
+        wave_sync();
+    }
     const uint32_t *blk0 = J.dec + (int64_t)blk * 64 * 64;
     const int64_t cstride = J.dec_ncw * 64;
     int lr = 0;                                          // lane index holding the traced state
@@ -527,15 +536,39 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     // wave in flight while one is walked): the walk itself is short, the loads are not
     u32x4 ra[16], rb[16], rc[16];
     auto ld = [&](u32x4 (&r)[16], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
-    ld(ra, nch - 1);
-    ld(rb, nch - 2);
-    for (int ch = nch - 1; ch >= 0; ch--) {
-        uint32_t *cur = stage[ch & 1];
-        const int slot = (nch - 1 - ch) % 3;
-        if (slot == 0) { tb_stage(cur, ra, lane); wave_sync(); ld(ra, ch - 3); }
-        else if (slot == 1) { tb_stage(cur, rb, lane); wave_sync(); ld(rb, ch - 3); }
-        else { tb_stage(cur, rc, lane); wave_sync(); ld(rc, ch - 3); }
-        if (ch == nch - 1) ld(rc, ch - 2);
+    // Decoded bits leave in groups of TB_GROUP chunks (240 bytes per codeword, 16-byte
+    // stores): vector-memory stores pending beside the decision prefetches make the
+    // compiler wait for every outstanding load (vmcnt(0)), so they come rarely.
+    uint32_t gb[TB_GROUP];
+#pragma unroll
+    for (int i = 0; i < TB_GROUP; i++) gb[i] = 0;
+    const bool al16 = (((uintptr_t)J.out | (uintptr_t)J.out_stride) & 15) == 0;
+    auto flush = [&](int g) {
+        const int tg = WS * TB_GROUP * g;
+        if (!act || tg >= N) return;
+        if (al16 && tg + WS * TB_GROUP <= N) {
+#pragma unroll
+            for (int q = 0; q < WS * TB_GROUP / 16; q++) {
+                uint32_t d[4];
+#pragma unroll
+                for (int e = 0; e < 4; e++) {
+                    const int b = 16 * q + 4 * e, c = b / WS, r = b % WS;    // compile-time
+                    uint32_t x = gb[c] >> r;
+                    if (r > WS - 4) x |= gb[c + 1] << (WS - r);
+                    d[e] = ((x & 0xFu) * 0x204081u) & 0x01010101u;           // 4 bits -> 4 bytes
+                }
+                *(uint4 *)(out + tg + 16 * q) = make_uint4(d[0], d[1], d[2], d[3]);
+            }
+        } else {                                         // the codeword's last group
+#pragma unroll
+            for (int k = 0; k < TB_GROUP; k++) {
+                const int base = tg + WS * k, nk = min(WS, N - base);
+                for (int i = 0; i < nk; i++) out[base + i] = (uint8_t)((gb[k] >> i) & 1u);
+            }
+        }
+    };
+    // the walk of chunk ch over its staged words
+    auto walk = [&](int ch, const uint32_t *cur) {
         const uint32_t *mine = cur + lane * TB_ROW;
         const int t0 = ch * WS;
         uint32_t w = 0;                                  // decoded bits of the chunk, step t0+k at bit k
@@ -587,21 +620,42 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
                 }
             }
         }
-        if (act && t0 < N) {
-            if (J.prbs) {                                // energy dispersal bits t0 .. t0+29
-                const int wi = t0 >> 5, sh = t0 & 31;
-                const uint32_t lo = J.prbs_words[wi], hi = J.prbs_words[wi + 1];
-                w ^= sh ? (lo >> sh) | (hi << (32 - sh)) : lo;
-            }
-            if (t0 + WS <= N) {
+        if (J.prbs) {                                    // energy dispersal bits t0 .. t0+29
+            const int wi = t0 >> 5, sh = t0 & 31;
+            const uint32_t lo = prbs_l[wi], hi = prbs_l[wi + 1];
+            w ^= (sh ? (lo >> sh) | (hi << (32 - sh)) : lo) & 0x3FFFFFFFu;
+        }
+        // the chunk's 30 bits join the group buffer (gb[k] = chunk TB_GROUP*g + k once
+        // the group's first chunk arrives; the walk runs downwards)
 #pragma unroll
-                for (int e = 0; e < WS / 2; e++)         // 2 bits -> 2 bytes (t0 is even)
-                    *(uint16_t *)(out + t0 + 2 * e) = (uint16_t)(((w >> (2 * e)) & 1u) | (((w >> (2 * e + 1)) & 1u) << 8));
-            } else {
-                for (int i = 0; t0 + i < N; i++) out[t0 + i] = (uint8_t)((w >> i) & 1u);
-            }
+        for (int i = TB_GROUP - 1; i > 0; i--) gb[i] = gb[i - 1];
+        gb[0] = w;
+        if (ch % TB_GROUP == 0) {
+            flush(ch / TB_GROUP);
+            // no store left pending: the decision prefetches' waits stay exact
+            __builtin_amdgcn_s_waitcnt(0x0F70);          // vmcnt(0) expcnt(7) lgkmcnt(15)
         }
         wave_sync();
+    };
+    // ring of three register sets, unrolled so every set is a fixed register range: the
+    // wait before staging a set then covers only its own loads, not the two chunks
+    // still in flight behind it
+    auto chunk = [&](u32x4 (&r)[16], int ch) {
+        uint32_t *cur = stage[ch & 1];
+        tb_stage(cur, r, lane);
+        wave_sync();
+        ld(r, ch - 3);
+        walk(ch, cur);
+    };
+    ld(ra, nch - 1);
+    ld(rb, nch - 2);
+    ld(rc, nch - 3);
+    for (int ch = nch - 1; ch >= 0; ch -= 3) {
+        chunk(ra, ch);
+        if (ch < 1) break;
+        chunk(rb, ch - 1);
+        if (ch < 2) break;
+        chunk(rc, ch - 2);
     }
 }
 
@@ -622,13 +676,15 @@ __global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
 template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     __shared__ uint32_t stage[2][TB_WORDS];
-    tb_body<KIND>(J, blockIdx.x, stage);
+    __shared__ uint32_t prbs_l[TB_PRBS];
+    tb_body<KIND>(J, blockIdx.x, stage, prbs_l);
 }
 template <int KA, int KB>
 __global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) {
     __shared__ uint32_t stage[2][TB_WORDS];
-    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, stage);
-    else tb_body<KB>(B, blockIdx.x - nba, stage);
+    __shared__ uint32_t prbs_l[TB_PRBS];
+    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, stage, prbs_l);
+    else tb_body<KB>(B, blockIdx.x - nba, stage, prbs_l);
 }
 
 // FIB CRC check (dab-constants.h:310-340): invert the 16 CRC bits in place, run
