@@ -119,6 +119,19 @@ int         dabgpu_event_record(dabgpu_ctx *ctx, int slot);
 int         dabgpu_kernel_errors(dabgpu_ctx *ctx);
 int         dabgpu_event_elapsed(dabgpu_ctx *ctx, int slot_a, int slot_b, float *ms);
 
+/* ---- recorded IQ formats ---------------------------- */
+/* Convert device-resident recorded samples to the interleaved cf32 IQ every OFDM
+ * entry point reads, with the reference file readers' scaling:
+ *   DABGPU_IQ_U8   .raw: rawFiles::getSamples (rawfiles.cpp:100-118),
+ *                  I/Q = float(x - 128) / 128.0
+ *   DABGPU_IQ_S16  .sdr: 2-channel PCM16 WAV at 2.048 MHz, wavFiles (wavfiles.cpp:
+ *                  64-69, readBuffer) through libsndfile's sf_readf_float: x / 32768
+ * n_pairs I/Q pairs: src_d holds 2*n_pairs values, iq_d receives 2*n_pairs floats.
+ * Asynchronous on the context stream (dabgpu_sync to wait). */
+#define DABGPU_IQ_U8   1
+#define DABGPU_IQ_S16  2
+int dabgpu_iq_convert(dabgpu_ctx *ctx, int format, const void *src_d, int64_t n_pairs, float *iq_d);
+
 /* ---- OFDM front end (L3) ---------------------------------------------- */
 
 /* phaseReference::findIndex batched (phasereference.cpp:60-88): for each of n

@@ -133,6 +133,7 @@ hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &f
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
+hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_t n_values, float *dst);
 hipError_t launch_rs(hipStream_t st, const uint8_t *in, int n, const uint8_t *tabs, uint8_t *out, int16_t *ret);
 
 }  // namespace dab

@@ -416,6 +416,14 @@ int dabgpu_memcpy_d2h(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
+int dabgpu_iq_convert(dabgpu_ctx *c, int format, const void *src, int64_t n_pairs, float *iq) {
+    if (!c || (!src && n_pairs > 0) || (!iq && n_pairs > 0) || n_pairs < 0) return fail(DABGPU_E_ARG, "bad args");
+    if (format != DABGPU_IQ_U8 && format != DABGPU_IQ_S16) return fail(DABGPU_E_ARG, "unknown IQ format %d", format);
+    // the vector path reads 16 B per 16 values: the source must be 16-byte aligned
+    if (((uintptr_t)src & 15) || ((uintptr_t)iq & 15)) return fail(DABGPU_E_ARG, "IQ buffers must be 16-byte aligned");
+    HIPCHK(launch_iq_convert(c->stream, format, src, 2 * n_pairs, iq));
+    return 0;
+}
 int dabgpu_memset_d(dabgpu_ctx *c, void *dst, int value, size_t bytes) {
     if (!c) return fail(DABGPU_E_ARG, "null ctx");
     HIPCHK(hipMemsetAsync(dst, value, bytes, c->stream));

@@ -274,3 +274,49 @@ hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, i
 }
 
 }  // namespace dab
+
+namespace dab {
+
+// Recorded IQ to cf32 (dabgpu.h, DABGPU_IQ_*): one thread per 16 input values, 16-byte
+// loads (u8) / 2 x 16-byte loads (s16) and 4 x 16-byte stores; HBM-bound
+// (5 or 6 bytes per value).  The tail (n_values % 16) is done value by value.
+template <int FMT>
+__global__ __launch_bounds__(256) void k_iq_convert(const void *__restrict__ src, int64_t n_values,
+                                                    float *__restrict__ dst) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t v0 = i * 16;
+    if (v0 >= n_values) return;
+    float f[16];
+    if (v0 + 16 <= n_values) {
+        if constexpr (FMT == DABGPU_IQ_U8) {
+            const uint4 w = ((const uint4 *)src)[i];
+            const uint32_t u[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++) f[k] = (float)((int)((u[k >> 2] >> (8 * (k & 3))) & 0xFFu) - 128) / 128.0f;
+        } else {
+            const uint4 a = ((const uint4 *)src)[2 * i], b = ((const uint4 *)src)[2 * i + 1];
+            const uint32_t u[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int k = 0; k < 16; k++) f[k] = (float)(int16_t)(u[k >> 1] >> (16 * (k & 1))) * (1.0f / 32768.0f);
+        }
+#pragma unroll
+        for (int q = 0; q < 4; q++) ((float4 *)dst)[4 * i + q] = make_float4(f[4 * q], f[4 * q + 1], f[4 * q + 2], f[4 * q + 3]);
+    } else {
+        for (int64_t v = v0; v < n_values; v++) {
+            if constexpr (FMT == DABGPU_IQ_U8) dst[v] = (float)((int)((const uint8_t *)src)[v] - 128) / 128.0f;
+            else dst[v] = (float)((const int16_t *)src)[v] * (1.0f / 32768.0f);
+        }
+    }
+}
+
+hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_t n_values, float *dst) {
+    if (n_values <= 0) return hipSuccess;
+    const int64_t threads = (n_values + 15) / 16;
+    const dim3 grid((unsigned)((threads + 255) / 256));
+    if (format == DABGPU_IQ_U8) hipLaunchKernelGGL(k_iq_convert<DABGPU_IQ_U8>, grid, dim3(256), 0, st, src, n_values, dst);
+    else if (format == DABGPU_IQ_S16) hipLaunchKernelGGL(k_iq_convert<DABGPU_IQ_S16>, grid, dim3(256), 0, st, src, n_values, dst);
+    else return hipErrorInvalidValue;
+    return hipGetLastError();
+}
+
+}  // namespace dab

@@ -81,6 +81,7 @@ def lib() -> C.CDLL:
             "dabgpu_alloc": ([vp, sz, C.POINTER(vp)], i32), "dabgpu_free": ([vp, vp], i32),
             "dabgpu_memcpy_h2d": ([vp, vp, vp, sz], i32), "dabgpu_memcpy_d2h": ([vp, vp, vp, sz], i32),
             "dabgpu_memset_d": ([vp, vp, i32, sz], i32),
+            "dabgpu_iq_convert": ([vp, i32, vp, i64, vp], i32),
             "dabgpu_event_record": ([vp, i32], i32),
             "dabgpu_kernel_errors": ([vp], i32),
             "dabgpu_event_elapsed": ([vp, i32, i32, C.POINTER(C.c_float)], i32),
@@ -118,6 +119,65 @@ def _chk(rc: int, what: str) -> None:
 
 def _p(a: np.ndarray) -> C.c_void_p:
     return C.c_void_p(a.ctypes.data)
+
+
+IQ_U8, IQ_S16 = 1, 2   # dabgpu_iq_convert formats
+
+
+def read_raw(path: str) -> np.ndarray:
+    """.raw recording (rawfiles.cpp): interleaved unsigned 8-bit I/Q, no header.
+    Returns the bytes memory-mapped (an odd trailing byte is dropped)."""
+    a = np.memmap(path, dtype=np.uint8, mode="r")
+    return a[: a.size & ~1]
+
+
+def read_sdr(path: str) -> np.ndarray:
+    """.sdr recording (wavfiles.cpp:56-69): a WAV file with 2 channels (I, Q) of
+    PCM16 at 2048000 samples/s.  Returns the interleaved int16 samples
+    memory-mapped; raises ValueError for any other WAV layout, as the reference
+    refuses it ("This is not a recorded dab file")."""
+    import struct
+    with open(path, "rb") as f:
+        head = f.read(12)
+        if len(head) < 12 or head[:4] != b"RIFF" or head[8:12] != b"WAVE":
+            raise ValueError(f"{path}: not a RIFF/WAVE file")
+        fmt = None
+        off = 12
+        while True:
+            ck = f.read(8)
+            if len(ck) < 8:
+                raise ValueError(f"{path}: no data chunk")
+            cid, n = ck[:4], struct.unpack("<I", ck[4:])[0]
+            off += 8
+            if cid == b"fmt ":
+                b = f.read(n)
+                tag, ch, rate, _, _, bits = struct.unpack("<HHIIHH", b[:16])
+                if tag == 0xFFFE and n >= 26:              # WAVE_FORMAT_EXTENSIBLE: subformat GUID
+                    tag = struct.unpack("<H", b[24:26])[0]
+                fmt = (tag, ch, rate, bits)
+            elif cid == b"data":
+                if fmt is None:
+                    raise ValueError(f"{path}: data before fmt chunk")
+                if fmt != (1, 2, 2048000, 16):
+                    raise ValueError(f"{path}: not a recorded DAB file (format/channels/rate/bits {fmt}); "
+                                     "need PCM16, 2 channels, 2048000 Hz")
+                size = os.path.getsize(path)
+                n = min(n, size - off) & ~3
+                return np.memmap(path, dtype="<i2", mode="r", offset=off, shape=(n // 2,))
+            else:
+                f.seek(n + (n & 1), 1)
+            off += n + (n & 1)
+
+
+def write_sdr(path: str, iq_s16: np.ndarray) -> None:
+    """write interleaved int16 I/Q as an .sdr WAV (2 channels, PCM16, 2048000 Hz):
+    the recording format of gui.cpp:880-883"""
+    import wave
+    with wave.open(path, "wb") as w:
+        w.setnchannels(2)
+        w.setsampwidth(2)
+        w.setframerate(2048000)
+        w.writeframes(np.ascontiguousarray(iq_s16, dtype="<i2").tobytes())
 
 
 class DevBuf:
@@ -175,6 +235,35 @@ class Context:
 
     def sync(self) -> None:
         _chk(lib().dabgpu_sync(self.h), "sync")
+
+    def iq_convert(self, fmt: int, src: "DevBuf", n_pairs: int, dst: "DevBuf", src_off: int = 0,
+                   dst_off: int = 0) -> None:
+        """dabgpu_iq_convert: recorded samples (IQ_U8 / IQ_S16) in src -> cf32 in dst"""
+        _chk(lib().dabgpu_iq_convert(self.h, fmt, C.c_void_p(src.ptr.value + src_off), n_pairs,
+                                     C.c_void_p(dst.ptr.value + dst_off)), "dabgpu_iq_convert")
+
+    def load_iq_file(self, path: str, max_pairs: Optional[int] = None, chunk_pairs: int = 1 << 25):
+        """Read a .raw (u8) or .sdr (WAV PCM16) recording into HBM as interleaved cf32,
+        converting on the GPU; streamed in chunks (host memory stays at one chunk).
+        Returns (DevBuf, n_pairs)."""
+        if path.endswith(".raw"):
+            src, fmt, w = read_raw(path), IQ_U8, 1
+        else:
+            src, fmt, w = read_sdr(path), IQ_S16, 2
+        n = src.size // 2
+        if max_pairs is not None:
+            n = min(n, int(max_pairs))
+        dst = self.buf(max(8 * n, 16))
+        stage = self.buf(2 * w * min(n, chunk_pairs) + 16)
+        try:
+            for p0 in range(0, n, chunk_pairs):
+                m = min(chunk_pairs, n - p0)
+                stage.upload(np.ascontiguousarray(src[2 * p0: 2 * (p0 + m)]))
+                self.iq_convert(fmt, stage, m, dst, dst_off=8 * p0)
+                self.sync()
+        finally:
+            stage.free()
+        return dst, n
 
     def check(self) -> None:
         """raise if a kernel refused out-of-bounds work since the last check"""

@@ -1,0 +1,57 @@
+"""Recorded-IQ file formats, host side: the .sdr WAV header check
+of wavFiles (wavfiles.cpp:56-69: 2 channels at 2048000 Hz, else "not a recorded dab
+file") and the .raw byte stream of rawFiles (rawfiles.cpp:100-118).  The GPU
+conversion itself is tested in test_gpu_formats.py."""
+import os
+import wave
+
+import numpy as np
+import pytest
+
+
+def test_sdr_roundtrip(tmp_path):
+    import dabamd
+    rng = np.random.default_rng(3)
+    iq = rng.integers(-32768, 32768, 2 * 1001, dtype=np.int16)
+    p = str(tmp_path / "x.sdr")
+    dabamd.write_sdr(p, iq)
+    got = dabamd.read_sdr(p)
+    assert got.dtype == np.dtype("<i2") and np.array_equal(np.asarray(got), iq)
+
+
+@pytest.mark.parametrize("ch,rate,width", [(1, 2048000, 2), (2, 48000, 2), (2, 2048000, 1)])
+def test_sdr_rejects_other_layouts(tmp_path, ch, rate, width):
+    import dabamd
+    p = str(tmp_path / "bad.wav")
+    with wave.open(p, "wb") as w:
+        w.setnchannels(ch)
+        w.setsampwidth(width)
+        w.setframerate(rate)
+        w.writeframes(b"\0" * (ch * width * 16))
+    with pytest.raises(ValueError):
+        dabamd.read_sdr(p)
+
+
+def test_sdr_skips_unknown_chunks(tmp_path):
+    """a LIST chunk between fmt and data (common in recorder output) is skipped"""
+    import dabamd
+    import struct
+    iq = np.arange(-8, 8, dtype=np.int16)
+    fmt = struct.pack("<HHIIHH", 1, 2, 2048000, 2048000 * 4, 4, 16)
+    lst = b"INFOtest!"                                       # odd size: padded
+    data = iq.tobytes()
+    body = b"WAVE" + b"fmt " + struct.pack("<I", len(fmt)) + fmt + b"LIST" + struct.pack("<I", len(lst)) + lst + b"\0" \
+        + b"data" + struct.pack("<I", len(data)) + data
+    p = str(tmp_path / "list.sdr")
+    with open(p, "wb") as f:
+        f.write(b"RIFF" + struct.pack("<I", len(body)) + body)
+    assert np.array_equal(np.asarray(dabamd.read_sdr(p)), iq)
+
+
+def test_raw_drops_odd_byte(tmp_path):
+    import dabamd
+    p = str(tmp_path / "x.raw")
+    b = np.arange(11, dtype=np.uint8)
+    b.tofile(p)
+    got = dabamd.read_raw(p)
+    assert got.size == 10 and np.array_equal(np.asarray(got), b[:10])
