@@ -44,12 +44,28 @@ def dist_setup(n_gpus):
     if world > 1:
         import torch
         import torch.distributed as td
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        # RCCL when every local rank has its own GPU (the driver's 1..8-GPU node runs);
+        # gloo when ranks share one (a rehearsal of the N > 1 path on a 1-GPU box) or
+        # there is no GPU.  The path itself has no collective: only the start/stop
+        # barriers and the max-over-ranks time go through torch.distributed.
+        ngpu = torch.cuda.device_count()
+        lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
+        backend = os.environ.get("DAB_DIST_BACKEND") or ("nccl" if ngpu >= lws and ngpu > 0 else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         td.init_process_group(backend=backend)
         dist = td
     return rank, local, world, dist
+
+
+def rank_device(local):
+    """GPU of a local rank (ranks share GPUs round-robin when there are fewer GPUs)"""
+    try:
+        import torch
+        n = torch.cuda.device_count()
+    except ImportError:
+        n = 1
+    return local % max(n, 1)
 
 
 def rank_seed0(rank, ensembles):
@@ -177,7 +193,7 @@ def main():
     E, F = args.ensembles or E_default, args.frames
     total_frames = F * (args.warmup + args.steps + 1) + 1   # +1 step: the profiled pass
     ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0)
-    ctx = dabamd.Context(local)
+    ctx = dabamd.Context(rank_device(local))
     stride = ens.length
     # generated in groups straight into HBM: host memory stays at one group (~2 GB)
     # however many ensembles and frames the run decodes
