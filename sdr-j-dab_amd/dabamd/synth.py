@@ -19,7 +19,7 @@ class SynthSubch(C.Structure):
 class SynthCfg(C.Structure):
     _fields_ = [("n_frames", C.c_int32), ("pre_offset", C.c_int32), ("snr_db", C.c_float),
                 ("cfo_hz", C.c_float), ("amplitude", C.c_float), ("n_subch", C.c_int32),
-                ("subch", C.POINTER(SynthSubch))]
+                ("subch", C.POINTER(SynthSubch)), ("figs", C.c_int32)]
 
 
 def lib() -> C.CDLL:
@@ -48,12 +48,12 @@ class Ensemble:
     protLevel, uep, dabplus) -- uep=1 for UEP (uepFlag 0 in the reference)."""
 
     def __init__(self, n_frames: int, subch: Sequence[tuple] = (), pre_offset: int = 50000,
-                 snr_db: float = 300.0, cfo_hz: float = 0.0, amplitude: float = 1.0):
+                 snr_db: float = 300.0, cfo_hz: float = 0.0, amplitude: float = 1.0, figs: bool = False):
         self.n_frames = n_frames
         self.subch = [SynthSubch(*s) for s in subch]
         self._arr = (SynthSubch * max(1, len(self.subch)))(*self.subch)
         self.cfg = SynthCfg(n_frames, pre_offset, snr_db, cfo_hz, amplitude, len(self.subch),
-                            C.cast(self._arr, C.POINTER(SynthSubch)))
+                            C.cast(self._arr, C.POINTER(SynthSubch)), int(figs))
         self.length = lib().dabsynth_stream_len(C.byref(self.cfg))
         self.maxbits = 24 * max([s.bitRate for s in self.subch] + [8])
 

@@ -2,6 +2,7 @@
 // Input generator for tests/bench; not on the decode path.
 #include "dabsynth.h"
 #include <cmath>
+#include <cstdio>
 #include <cstring>
 #include <cstdlib>
 #include <vector>
@@ -309,6 +310,75 @@ void dabsynth_puncture_fic(const uint8_t *mother, uint8_t *out) {
     for (int j = 0; j < 24; j++, ic++) if (kPIX[j]) out[oc++] = mother[ic];
 }
 
+// ETSI EN 300 401 table 8 index of a UEP (bit rate, level): rows per bit rate from
+// level 5 down (56 kbit/s has no level 1; 320 no 3 and 1; 384 only 5, 3, 1)
+static int uep_table_index(int kbps, int level) {
+    static const struct { int kbps; int levels[5]; int n; } g[] = {
+        {32, {5, 4, 3, 2, 1}, 5}, {48, {5, 4, 3, 2, 1}, 5}, {56, {5, 4, 3, 2, 0}, 4}, {64, {5, 4, 3, 2, 1}, 5},
+        {80, {5, 4, 3, 2, 1}, 5}, {96, {5, 4, 3, 2, 1}, 5}, {112, {5, 4, 3, 2, 0}, 4}, {128, {5, 4, 3, 2, 1}, 5},
+        {160, {5, 4, 3, 2, 1}, 5}, {192, {5, 4, 3, 2, 1}, 5}, {224, {5, 4, 3, 2, 1}, 5}, {256, {5, 4, 3, 2, 1}, 5},
+        {320, {5, 4, 2, 0, 0}, 3}, {384, {5, 3, 1, 0, 0}, 3}};
+    int idx = 0;
+    for (const auto &r : g)
+        for (int k = 0; k < r.n; k++, idx++)
+            if (r.kbps == kbps && r.levels[k] == level) return idx;
+    return -1;
+}
+
+namespace {
+struct BitWriter {
+    uint8_t *b;
+    int pos = 0;
+    void put(uint32_t v, int n) {
+        for (int i = n - 1; i >= 0; i--, pos++)
+            if ((v >> i) & 1) b[pos >> 3] |= (uint8_t)(0x80 >> (pos & 7));
+    }
+};
+}  // namespace
+
+// FIB number n of an ensemble with FIGs (cfg->figs): item n mod (1 + 2 * n_subch)
+static void make_fig_fib(const dabsynth_cfg *cfg, int64_t n, uint8_t *fib) {
+    uint8_t bytes[32];
+    std::memset(bytes, 0, sizeof bytes);
+    BitWriter w{bytes};
+    const int items = 1 + 2 * cfg->n_subch;
+    const int j = (int)(n % items);
+    auto label = [&](const char *l) {
+        for (int i = 0; i < 16; i++) w.put((uint8_t)l[i], 8);
+        w.put(0xFF00, 16);
+    };
+    if (j == 0) {                                          // FIG 1/0 ensemble label
+        w.put(1, 3), w.put(21, 5), w.put(0, 4), w.put(0, 1), w.put(0, 3), w.put(0xE1C3, 16);
+        label("SYNTH ENSEMBLE  ");
+    } else if (j & 1) {                                    // FIG 1/1 service label
+        const int i = (j - 1) / 2;
+        char l[17];
+        std::snprintf(l, sizeof l, "SERVICE %02d      ", i % 100);
+        w.put(1, 3), w.put(21, 5), w.put(0, 4), w.put(0, 1), w.put(1, 3), w.put(0xC000 + i, 16);
+        label(l);
+    } else {                                               // FIG 0/1 + FIG 0/2
+        const int i = j / 2 - 1;
+        const dabsynth_subch &sc = cfg->subch[i];
+        const int tix = sc.uep ? uep_table_index(sc.bitRate, sc.protLevel) : -1;
+        const bool shortform = sc.uep && tix >= 0;
+        w.put(0, 3), w.put(shortform ? 4 : 5, 5), w.put(0, 3), w.put(1, 5);
+        w.put(i, 6), w.put(sc.startAddr, 10);
+        if (shortform) {
+            w.put(0, 1), w.put(0, 1), w.put(tix, 6);
+        } else {
+            w.put(1, 1), w.put((sc.protLevel & 0200) ? 1 : 0, 3), w.put((sc.protLevel & 7) - 1, 2), w.put(sc.length, 10);
+        }
+        w.put(0, 3), w.put(6, 5), w.put(0, 3), w.put(2, 5);
+        w.put(0xC000 + i, 16), w.put(0, 1), w.put(0, 3), w.put(1, 4);
+        w.put(0, 2), w.put(sc.dabplus ? 63 : 0, 6), w.put(i, 6), w.put(1, 1), w.put(0, 1);
+    }
+    for (int k = (w.pos + 7) >> 3; k < 30; k++) bytes[k] = 0xFF;    // end marker / padding
+    const uint16_t c = (uint16_t)~crc_ccitt(bytes, 30);
+    bytes[30] = (uint8_t)(c >> 8);
+    bytes[31] = (uint8_t)(c & 0xff);
+    for (int i = 0; i < 256; i++) fib[i] = (uint8_t)((bytes[i >> 3] >> (7 - (i & 7))) & 1);
+}
+
 void dabsynth_make_fib(uint64_t *st, uint8_t *fib) {
     Rng rng(*st);
     uint8_t bytes[32];
@@ -393,7 +463,10 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
         std::vector<uint8_t> ficsym(9216);
         for (int blk = 0; blk < 4; blk++) {
             uint8_t fib[768], mother[3096], punct[2304];
-            for (int q = 0; q < 3; q++) dabsynth_make_fib(&fib_state, fib + 256 * q);
+            for (int q = 0; q < 3; q++) {
+                if (cfg->figs) make_fig_fib(cfg, ((int64_t)(f + 1) * 4 + blk) * 3 + q, fib + 256 * q);
+                else dabsynth_make_fib(&fib_state, fib + 256 * q);
+            }
             if (fic_bits && f >= 0) std::memcpy(&fic_bits[((size_t)f * 4 + blk) * 768], fib, 768);
             for (int i = 0; i < 768; i++) fib[i] ^= t.prbs[i];
             dabsynth_conv_encode(fib, 768, mother);

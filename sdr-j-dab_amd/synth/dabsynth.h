@@ -38,6 +38,11 @@ typedef struct {
     float   amplitude;   /* RMS of the OFDM signal */
     int32_t n_subch;
     const dabsynth_subch *subch;
+    int32_t figs;        /* 0: FIBs of random bytes (with CRC); 1: FIGs describing the
+                            ensemble -- FIG 1/0 label "SYNTH ENSEMBLE", per subchannel i
+                            FIG 0/1 (sub-channel i), FIG 0/2 (service 0xC000+i, one audio
+                            component, ASCTy 63 for DAB+), FIG 1/1 label "SERVICE ii" --
+                            cycled one item per FIB */
 } dabsynth_cfg;
 
 /* total stream length in samples */

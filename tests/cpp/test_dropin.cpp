@@ -10,6 +10,7 @@
 
 #include "dab_oracle.h"
 #include "dabgpu_dropin.h"
+#include "fib_processor.h"
 #include "dabsynth.h"
 
 static int failures = 0;
@@ -192,6 +193,76 @@ int main() {
         CHECK(msc_n == 2 * (NC - 16) * 3 && msc_bad == 0, "MSC %d bad %d", msc_n, msc_bad);
         CHECK(sf_ok >= 2 * 2 * 3 && sf_bad == 0, "superframes ok %d bad %d", sf_ok, sf_bad);
         std::printf("ensembleDecoder: ok (%d FIBs, %d MSC CIF-subchannels, %d superframes)\n", fib_n, msc_n, sf_ok);
+    }
+    // a functional ficHandler: the GPU-decoded FIBs of an ensemble that describes
+    // itself (FIG 0/1, 0/2, 1/0, 1/1) configure the MSC decoder through
+    // fib_processor::dataforAudioService, and that decoder reproduces the MSC bits
+    {
+        dabsynth_subch sc[3] = {{0, 96, 128, 3, 1, 0}, {96, 48, 64, 0103, 0, 1}, {144, 54, 64, 0201, 0, 0}};
+        dabsynth_cfg cfg;
+        std::memset(&cfg, 0, sizeof cfg);
+        const int F = 3, runs = 2;
+        cfg.n_frames = F * runs;
+        cfg.pre_offset = 50000;
+        cfg.snr_db = 30.0f;
+        cfg.amplitude = 1.0f;
+        cfg.n_subch = 3;
+        cfg.subch = sc;
+        cfg.figs = 1;
+        const int64_t n = dabsynth_stream_len(&cfg);
+        const int NC = 4 * F * runs, maxbits = 24 * 128;
+        std::vector<float> iq(2 * n);
+        std::vector<uint8_t> msc((size_t)NC * 3 * maxbits);
+        int64_t f0;
+        dabsynth_generate(&cfg, 555, iq.data(), nullptr, msc.data(), nullptr, &f0);
+        dabgpu::fib_processor fibs;
+        {   // pass 1: FIC only
+            dabgpu::ensembleDecoder::config ec;
+            ec.n_streams = 1;
+            ec.n_frames = F;
+            dabgpu::ensembleDecoder dec(ec);
+            int good = 0;
+            dec.on_fib([&](int, int64_t, int ficno, const uint8_t *bits, bool ok) {
+                if (ok) fibs.process_FIB(bits, (uint16_t)ficno), good++;
+            });
+            dec.load({(const dabgpu::DSPCOMPLEX *)iq.data()}, {n});
+            dec.acquire();
+            for (int r = 0; r < runs; r++) CHECK(dec.step(), "FIC pass step %d", r);
+            CHECK(good == 12 * F * runs, "FIC pass: %d good FIBs", good);
+        }
+        CHECK(fibs.ensembleName() == "SYNTH ENSEMBLE  ", "ensemble '%s'", fibs.ensembleName().c_str());
+        dabgpu::ensembleDecoder::config ec;
+        ec.n_streams = 1;
+        ec.n_frames = F;
+        for (int i = 0; i < 3; i++) {
+            char lab[17];
+            std::snprintf(lab, sizeof lab, "SERVICE %02d      ", i);
+            dabgpu::audiodata a;
+            const bool ok = fibs.kindofService(lab) == dabgpu::AUDIO_SERVICE && fibs.dataforAudioService(lab, &a);
+            CHECK(ok, "service %d from the FIC", i);
+            if (!ok) break;
+            CHECK(a.startAddr == sc[i].startAddr && a.length == sc[i].length && a.bitRate == sc[i].bitRate &&
+                      a.protLevel == sc[i].protLevel, "service %d subchannel", i);
+            ec.subch.push_back({a.startAddr, a.length, a.bitRate, a.protLevel, (int16_t)a.uepFlag,
+                                (int16_t)(a.ASCTy == 63 ? DABGPU_SUBCH_DABPLUS : 0)});
+        }
+        if (ec.subch.size() == 3) {   // pass 2: the services the FIC announced
+            dabgpu::ensembleDecoder dec(ec);
+            int msc_n = 0, msc_bad = 0, sf_ok = 0;
+            dec.on_msc([&](int, int64_t cif, int k, const uint8_t *bits, int nbits) {
+                msc_n++;
+                if (std::memcmp(bits, msc.data() + ((size_t)cif * 3 + k) * maxbits, nbits)) msc_bad++;
+            });
+            dec.on_superframe([&](int, int64_t, int, const dabgpu_superframe &info, const uint8_t *, int) {
+                sf_ok += info.status == 3;
+            });
+            dec.load({(const dabgpu::DSPCOMPLEX *)iq.data()}, {n});
+            dec.acquire();
+            for (int r = 0; r < runs; r++) CHECK(dec.step(), "MSC pass step %d", r);
+            CHECK(msc_n == (NC - 16) * 3 && msc_bad == 0, "self-configured MSC %d bad %d", msc_n, msc_bad);
+            CHECK(sf_ok >= 1, "self-configured DAB+ superframes %d", sf_ok);
+            std::printf("fib_processor + ensembleDecoder: ok (%d MSC CIF-subchannels, %d superframes)\n", msc_n, sf_ok);
+        }
     }
     if (failures) {
         std::printf("DROPIN FAILED (%d)\n", failures);
