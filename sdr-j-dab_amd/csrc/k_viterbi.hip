@@ -62,6 +62,8 @@ __device__ __forceinline__ void wave_sync() {
 // Per-codeword source, resolved once per wave.
 struct Src {
     const int16_t *base;   // first input element (SRC_MSC: the stream's ring)
+    __amdgpu_buffer_rsrc_t rs;   // buffer over the readable elements: 32-bit offsets, and
+                                 // reads past its end (erasures, empty delay line) return 0
     int prof;              // profile index
     int row;               // output / decision row of this codeword
     bool valid;
@@ -114,6 +116,7 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
         wave_sync();
     }
     if (c.valid && J.valid && !J.valid[c.row]) c.valid = false;
+    int64_t nrec = 0;                                  // readable bytes from base
     if constexpr (KIND != SRC_MSC) {
         if (c.valid) {
             const Profile &P = J.prof[c.prof];
@@ -123,8 +126,18 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
                 if (lane == 0) atomicOr(J.err, KERR_VITERBI);
                 c.valid = false;
             }
+            nrec = 2 * need;
         }
+    } else {
+        nrec = 2 * (int64_t)J.ring * FRAME_SOFT;        // the stream's ring (rowoff checked above)
     }
+    // wave-uniform by construction; readfirstlane keeps the descriptor in SGPRs
+    const uint64_t b = (uint64_t)(uintptr_t)c.base;
+    // (readfirstlane returns int: widen through uint32_t, no sign extension)
+    const uint64_t bu = ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32)) << 32) |
+                        (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+    const int nu = __builtin_amdgcn_readfirstlane(c.valid ? (int)nrec : 0);
+    c.rs = __builtin_amdgcn_make_buffer_rsrc((void *)(uintptr_t)bu, (short)0, nu, 0x00020000);
     return c;
 }
 
@@ -215,8 +228,8 @@ __device__ __forceinline__ void load4(const Src &c, const int32_t *rowoff, const
             k = k && ro >= 0;                         // delay line still empty: zero
             off = ro + idx[e];
         }
-        const unsigned short v = (unsigned short)c.base[k ? off : 0];
-        s[e][H] = k ? v : (unsigned short)0;
+        // erasures read past the buffer's end: the hardware returns 0
+        s[e][H] = __builtin_amdgcn_raw_buffer_load_b16(c.rs, k ? 2 * off : 0x7FFFFFF0, 0, 0);
     }
 }
 
