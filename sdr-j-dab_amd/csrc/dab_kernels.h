@@ -23,6 +23,7 @@ struct OfdmTables {
     const int16_t *carrier_of_bin;   // [2048] carrier index of an FFT bin (mapper.cpp), -1 if none
     int32_t *err;           // device error word: kernels OR in DABGPU_KERR_* bits
 };
+constexpr int FRAME_SI_ON_DEVICE = 2;   // dabgpu_frame.flags bit (pipeline-internal)
 constexpr int KERR_FRAME = 1;      // frame descriptor outside its stream / bad NCO phase
 constexpr int KERR_VITERBI = 2;    // Viterbi source outside its buffer
 
@@ -121,8 +122,11 @@ hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *
                            int level, int32_t *si, float *mx, float *sm, bool general);
 hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
                          int16_t *corr, bool general);
+// si (optional): per-frame startIndex from k_prs_sync, used by frames flagged
+// FRAME_SI_ON_DEVICE (block0 and lp_data derived on the device)
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
-                        const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general);
+                        const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
+                        const int32_t *si = nullptr);
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
 hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
                           AcqResult *res);

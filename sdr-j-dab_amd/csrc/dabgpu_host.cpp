@@ -961,11 +961,30 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     const int n = (int)fr.size();
     progress = false;
     if (n == 0) return 0;
+    // Steady state (no stream runs the coarse AFC of processBlock_0): the demod of
+    // every predicted frame follows k_prs_sync on the device, which places each frame
+    // at its measured startIndex -- one host round trip per pass instead of two.
+    // Frames the replay below does not commit are re-predicted and decoded again.
+    bool fast = true;
+    for (const dabgpu_frame &d : fr) fast = fast && !(d.flags & 1);
+    if (fast)
+        for (dabgpu_frame &d : fr) d.flags |= FRAME_SI_ON_DEVICE;
     HIPCHK(hipMemcpyAsync(p->frames_d, fr.data(), sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
     HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
     HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
     std::vector<int32_t> si(n);
+    std::vector<float2> fc_all;
+    if (fast) {
+        fc_all.resize(n);
+        HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
+        const int kChunks = demod_chunks(n);
+        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general,
+                            p->si_d));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
+        HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n, p->fc_d));
+        HIPCHK(hipMemcpyAsync(fc_all.data(), p->fc_d, sizeof(float2) * n, hipMemcpyDeviceToHost, c->stream));
+    }
     HIPCHK(hipMemcpyAsync(si.data(), p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     if (int rc = kernel_errors(c)) return rc;
     // pass 1: windows.  A frame is usable if every earlier frame of its stream
@@ -1047,7 +1066,10 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     for (int k = 0; k < n2; k++) if (ok[idx[k]]) { idx3.push_back(idx[k]); fr3.push_back(fr2[k]); }
     const int n3 = (int)fr3.size();
     std::vector<float2> fc(n3);
-    if (n3) {
+    if (n3 && fast) {
+        for (int k = 0; k < n3; k++) fc[k] = fc_all[idx3[k]];   // demodulated above
+    } else if (n3) {
+        for (dabgpu_frame &d : fr3) d.flags &= ~FRAME_SI_ON_DEVICE;
         HIPCHK(hipMemcpyAsync(p->frames_d, fr3.data(), sizeof(dabgpu_frame) * n3, hipMemcpyHostToDevice, c->stream));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         const int kChunks = demod_chunks(n3);

@@ -155,7 +155,8 @@ template <bool GEN>
 __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2 *__restrict__ iq,
                                                     const dabgpu_frame *__restrict__ frames, int nchunks,
                                                     OfdmTables T, int16_t *__restrict__ soft,
-                                                    float *__restrict__ softf, float2 *__restrict__ fcpart) {
+                                                    float *__restrict__ softf, float2 *__restrict__ fcpart,
+                                                    const int32_t *__restrict__ si) {
     __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
     __shared__ int16_t st[2 * K + 2 * DT];
     __shared__ float2 fcw[DT / 64];
@@ -165,15 +166,31 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     __syncthreads();
     const int item = blockIdx.x;
     const int fi = item / nchunks, ch = item % nchunks;
-    const dabgpu_frame fr = frames[fi];
+    dabgpu_frame fr = frames[fi];
+    // FRAME_SI_ON_DEVICE: the frame starts where k_prs_sync found it (block0 = window +
+    // startIndex, ofdm-processor.cpp:360-368) -- no host round trip between the two;
+    // a frame whose sync failed or whose symbols are not all there yet is skipped
+    // (the host's replay does not commit it)
+    bool skip = false;
+    if (si && (fr.flags & FRAME_SI_ON_DEVICE)) {
+        const int32_t s = si[fi];
+        if (s < 0) {
+            skip = true;
+        } else {
+            fr.block0 = fr.window + s;
+            const int64_t m = ((int64_t)fr.lp_window - ((int64_t)TU + s) * (int64_t)fr.phase_a) % INPUT_RATE;
+            fr.lp_data = (int32_t)(m < 0 ? m + INPUT_RATE : m);
+            skip = fr.block0 + TU + (int64_t)NSYM * TS > fr.n_samples;
+        }
+    }
     const int per = (NSYM + nchunks - 1) / nchunks;
     const int l0 = 1 + ch * per, l1 = min(NSYM + 1, l0 + per);
     float2 fc = make_float2(0.0f, 0.0f);
     // frame_ok: every read inside the stream (the caller guarantees the descriptor)
     const bool ok = fr.window >= 0 && fr.block0 >= fr.window && fr.block0 + TU + (int64_t)NSYM * TS <= fr.n_samples &&
                     fr.lp_window >= 0 && fr.lp_window < INPUT_RATE && fr.lp_data >= 0 && fr.lp_data < INPUT_RATE;
-    if (!ok && t == 0) atomicOr(T.err, KERR_FRAME);
-    if (l0 <= NSYM && ok) {
+    if (!ok && !skip && t == 0) atomicOr(T.err, KERR_FRAME);
+    if (l0 <= NSYM && ok && !skip) {
         const float2 *s = iq + fr.iq_base;
         const int64_t dorg = fr.block0 + TU;           // first sample of segment B
         DemodTw tw;
@@ -269,15 +286,16 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
 }
 
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
-                        const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general) {
+                        const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
+                        const int32_t *si) {
     if (n <= 0) return hipSuccess;
     const dim3 grid(n * nchunks), block(DT);
     if (general)
         hipLaunchKernelGGL(k_demod_wg<true>, grid, block, 0, st, (const float2 *)iq, fr, nchunks, T, soft, softf,
-                           (float2 *)fcpart);
+                           (float2 *)fcpart, si);
     else
         hipLaunchKernelGGL(k_demod_wg<false>, grid, block, 0, st, (const float2 *)iq, fr, nchunks, T, soft, softf,
-                           (float2 *)fcpart);
+                           (float2 *)fcpart, si);
     return hipGetLastError();
 }
 
