@@ -169,8 +169,8 @@ def _cpu_worker(w, frames, budget_s, q, workload="c3"):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=12)
+    ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", choices=sorted(WORKLOADS), default="c3")
     ap.add_argument("--ensembles", type=int, default=0, help="ensembles per GPU (default: C3 64, C5 16)")
     ap.add_argument("--frames", type=int, default=24,

@@ -280,6 +280,7 @@ struct dabgpu_ctx {
     float *refarg = nullptr;
     uint8_t *dptab = nullptr;    // DAB+ tables (HostTables::dptab)
     int32_t *err = nullptr;      // device error word (KERR_* bits)
+    int32_t *h_err = nullptr;    // its pinned host copy (read after every synchronising pass)
     OfdmTables T{};
     // growable scratch
     void *scratch[8] = {};
@@ -302,9 +303,9 @@ enum { SC_DEC = 0, SC_PROF = 1, SC_I32 = 2, SC_FRAMES = 3, SC_FC = 4, SC_MISC = 
 
 // read (and clear) the device error word; call after a stream synchronisation
 static int kernel_errors(dabgpu_ctx *c) {
-    int32_t e = 0;
-    HIPCHK(hipMemcpyAsync(&e, c->err, sizeof e, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(c->h_err, c->err, sizeof(int32_t), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
+    const int32_t e = *c->h_err;
     if (!e) return 0;
     HIPCHK(hipMemsetAsync(c->err, 0, sizeof(int32_t), c->stream));
     return fail(DABGPU_E_BOUNDS, "kernel refused out-of-bounds work:%s%s", (e & KERR_FRAME) ? " frame descriptor" : "",
@@ -365,7 +366,8 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     c->T.w2048 = c->w2048;
     c->T.carrier_of_bin = c->carrier_bin;
     c->T.refarg = c->refarg;
-    if (hipMalloc((void **)&c->err, sizeof(int32_t)) != hipSuccess || hipMemset(c->err, 0, sizeof(int32_t)) != hipSuccess) {
+    if (hipMalloc((void **)&c->err, sizeof(int32_t)) != hipSuccess || hipMemset(c->err, 0, sizeof(int32_t)) != hipSuccess ||
+        hipHostMalloc((void **)&c->h_err, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {
         dabgpu_ctx_destroy(c);
         return fail(DABGPU_E_HIP, "error word alloc");
     }
@@ -381,6 +383,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
                     (void *)c->refarg, (void *)c->err, (void *)c->dptab})
         if (p) (void)hipFree(p);
+    if (c->h_err) (void)hipHostFree(c->h_err);
     for (auto p : c->scratch) if (p) (void)hipFree(p);
     for (auto e : c->ev) if (e) (void)hipEventDestroy(e);
     if (c->stream) (void)hipStreamDestroy(c->stream);
@@ -672,6 +675,12 @@ struct dabgpu_pipe {
     uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
     size_t dec_sz = 0;
     int64_t dec_fic_off = 0;                    // FIC decisions: words after the MSC's
+    // pinned host staging of the front end's per-pass copies (frame descriptors in,
+    // startIndex / FreqCorr out): DMA without the pageable bounce, each pass syncs
+    // before the buffers are touched again
+    dabgpu_frame *h_frames = nullptr;
+    int32_t *h_si = nullptr;
+    float2 *h_fc = nullptr;
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
     std::vector<int32_t> last_si;
@@ -784,6 +793,10 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->corr_d, sizeof(int16_t) * SF);
     A((void **)&p->fc_d, sizeof(float2) * SF);
     A((void **)&p->fcpart_d, sizeof(float2) * SF * kMaxChunks);
+    if (!rc && (hipHostMalloc((void **)&p->h_frames, sizeof(dabgpu_frame) * SF, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_si, sizeof(int32_t) * SF, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_fc, sizeof(float2) * SF, hipHostMallocDefault) != hipSuccess))
+        rc = fail(DABGPU_E_NOMEM, "pipe pinned staging");
     A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
     // MSC decisions, then the FIC's (both jobs of one run decode in one launch)
     const int64_t msc_words = p->NSUB > 0 ? dec_bytes(SF * 4 * p->NSUB, p->max_nbits) / 4 : 0;
@@ -856,6 +869,8 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
+    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc})
+        if (h) (void)hipHostFree(h);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d})
@@ -969,7 +984,8 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     for (const dabgpu_frame &d : fr) fast = fast && !(d.flags & 1);
     if (fast)
         for (dabgpu_frame &d : fr) d.flags |= FRAME_SI_ON_DEVICE;
-    HIPCHK(hipMemcpyAsync(p->frames_d, fr.data(), sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
+    memcpy(p->h_frames, fr.data(), sizeof(dabgpu_frame) * n);
+    HIPCHK(hipMemcpyAsync(p->frames_d, p->h_frames, sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
     HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
     HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
     HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
@@ -983,10 +999,12 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
                             p->si_d));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n, p->fc_d));
-        HIPCHK(hipMemcpyAsync(fc_all.data(), p->fc_d, sizeof(float2) * n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(p->h_fc, p->fc_d, sizeof(float2) * n, hipMemcpyDeviceToHost, c->stream));
     }
-    HIPCHK(hipMemcpyAsync(si.data(), p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    HIPCHK(hipMemcpyAsync(p->h_si, p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     if (int rc = kernel_errors(c)) return rc;
+    memcpy(si.data(), p->h_si, sizeof(int32_t) * n);
+    if (fast) memcpy(fc_all.data(), p->h_fc, sizeof(float2) * n);
     // pass 1: windows.  A frame is usable if every earlier frame of its stream
     // had the predicted startIndex; its own startIndex fixes block0.
     std::vector<char> ok(n, 0);
