@@ -482,19 +482,23 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 // LDS row per codeword: 64 words + 1 pad, so lanes tracing the same state (equal
 // lr, common when the streams carry similar data) read 64 different banks
 constexpr int TB_ROW = 65;
-constexpr int TB_WORDS = 64 * TB_ROW;      // one chunk of a wave's 64 codewords
+// codewords per traceback wave (32 would leave lanes 32..63 idle and halve each wave's
+// chunk and register ring for two waves per SIMD: measured slower, 0.41 vs 0.37 ms)
+constexpr int TB_CW = 64;
+constexpr int TB_LD = TB_CW / 4;            // 16-byte loads per lane per chunk
+constexpr int TB_WORDS = TB_CW * TB_ROW;    // one chunk of a wave's codewords
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TB_GROUP = 8;                 // chunks per output flush (240 bits per codeword)
 constexpr int TB_PRBS = 1024;              // PRBS words (fic-handler.cpp:100-108: 32768 bits)
-__device__ __forceinline__ void tb_load(u32x4 (&r)[16], const uint32_t *blk, int lane) {
+__device__ __forceinline__ void tb_load(u32x4 (&r)[TB_LD], const uint32_t *blk, int lane) {
     const u32x4 *q = (const u32x4 *)blk;
 #pragma unroll
-    for (int i = 0; i < 16; i++) r[i] = q[i * 64 + lane];
+    for (int i = 0; i < TB_LD; i++) r[i] = q[i * 64 + lane];
 }
-__device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[16], int lane) {
-    // r[i] = words 4q..4q+3 of the linear [64][64] block, q = i*64 + lane
+__device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[TB_LD], int lane) {
+    // r[i] = words 4q..4q+3 of the linear [TB_CW][64] block, q = i*64 + lane
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < TB_LD; i++) {
         const int q = i * 64 + lane, row = q >> 4, col = (q & 15) * 4;
         uint32_t *d = lds + row * TB_ROW + col;
         d[0] = r[i].x;
@@ -509,8 +513,8 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     // a latency-bound chain that issues little: first pick on its SIMD, so it keeps
     // its pace next to throughput-bound waves of other kernels (the next run's demod)
     __builtin_amdgcn_s_setprio(3);
-    const int lane = threadIdx.x, cw = blk * 64 + lane;
-    bool act = cw < J.n_cw;
+    const int lane = threadIdx.x, cw = blk * TB_CW + lane;
+    bool act = lane < TB_CW && cw < J.n_cw;
     int N = 0, prof = 0;
     if (act) {
         // validity and profile by output row (inverse of src_of's mapping)
@@ -542,13 +546,13 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
         for (int i = lane; i < nw; i += 64) prbs_l[i] = J.prbs_words[i];
         wave_sync();
     }
-    const uint32_t *blk0 = J.dec + (int64_t)blk * 64 * 64;
+    const uint32_t *blk0 = J.dec + (int64_t)blk * TB_CW * 64;
     const int64_t cstride = J.dec_ncw * 64;
     int lr = 0;                                          // lane index holding the traced state
     // decision chunks stream in through a 3-deep register ring (2 chunks = 32 KB per
     // wave in flight while one is walked): the walk itself is short, the loads are not
-    u32x4 ra[16], rb[16], rc[16];
-    auto ld = [&](u32x4 (&r)[16], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
+    u32x4 ra[TB_LD], rb[TB_LD], rc[TB_LD];
+    auto ld = [&](u32x4 (&r)[TB_LD], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
     // Decoded bits leave in groups of TB_GROUP chunks (240 bytes per codeword, 16-byte
     // stores): vector-memory stores pending beside the decision prefetches make the
     // compiler wait for every outstanding load (vmcnt(0)), so they come rarely.
@@ -582,7 +586,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     };
     // the walk of chunk ch over its staged words
     auto walk = [&](int ch, const uint32_t *cur) {
-        const uint32_t *mine = cur + lane * TB_ROW;
+        const uint32_t *mine = cur + (lane & (TB_CW - 1)) * TB_ROW;   // idle lanes walk a copy
         const int t0 = ch * WS;
         uint32_t w = 0;                                  // decoded bits of the chunk, step t0+k at bit k
         // two steps per LDS round trip: with the word of step k, read both candidate
@@ -653,7 +657,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     // ring of three register sets, unrolled so every set is a fixed register range: the
     // wait before staging a set then covers only its own loads, not the two chunks
     // still in flight behind it
-    auto chunk = [&](u32x4 (&r)[16], int ch) {
+    auto chunk = [&](u32x4 (&r)[TB_LD], int ch) {
         uint32_t *cur = stage[ch & 1];
         tb_stage(cur, r, lane);
         wave_sync();
@@ -742,7 +746,7 @@ hipError_t launch_acs(hipStream_t st, const VitJob &job) {
 hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
     if (job.dec_ncw < dec_rows(job.n_cw)) return hipErrorInvalidValue;
-    return launch_kind<TbK>(st, job, dim3((job.n_cw + 63) / 64));
+    return launch_kind<TbK>(st, job, dim3((job.n_cw + TB_CW - 1) / TB_CW));
 }
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     hipError_t e = launch_acs(st, job);
@@ -758,7 +762,7 @@ hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) 
 }
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
-    const int nba = (a.n_cw + 63) / 64, nbb = (b.n_cw + 63) / 64;
+    const int nba = (a.n_cw + TB_CW - 1) / TB_CW, nbb = (b.n_cw + TB_CW - 1) / TB_CW;
     hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(nba + nbb), dim3(64), 0, st, a, b, nba);
     return hipGetLastError();
 }
