@@ -248,8 +248,10 @@ int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
  * output buffers other than run r's unless this was called in between.  Also
  * reports a kernel that refused out-of-bounds work (DABGPU_E_BOUNDS). */
 int dabgpu_pipe_sync(dabgpu_pipe *p);
-/* per-stage kernel time of the last dabgpu_pipe_run (HIP events on the context
- * stream; enabling it adds one stream synchronisation at the end of each run) */
+/* per-stage kernel time (HIP events on each stage's stream, no synchronisation added):
+ * dabgpu_pipe_set_profiling(p, 1) times the last dabgpu_pipe_run, (p, 2) every run
+ * since the call (summed; launches counts them); 0 turns it off.  set_profiling
+ * waits for the pipeline's streams; dabgpu_pipe_timing waits for the recorded work. */
 #define DABGPU_STAGE_PRS      0   /* k_prs_sync   (findIndex)          */
 #define DABGPU_STAGE_BLOCK0   1   /* k_block0     (processBlock_0 AFC) */
 #define DABGPU_STAGE_DEMOD    2   /* k_demod      (processToken x 75)  */

@@ -708,7 +708,7 @@ struct dabgpu_pipe {
     int64_t run_idx = 0;
     Profile *ficprof_d = nullptr;
     // optional per-stage kernel timing (HIP events on the stage's stream)
-    bool profiling = false;
+    int profiling = 0;                          // 1: last run, 2: every run since enabled
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<int, int>> ev_rec;   // (stage, index of start event; end = +1)
     float stage_ms[DABGPU_NSTAGE] = {};
@@ -1163,7 +1163,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     for (int s = 0; s < S; s++) if (!p->st[s].synced) return fail(DABGPU_E_STATE, "stream %d not synchronised", s);
     p->last_frames.assign((size_t)S * F, dabgpu_frame());
     p->last_si.assign((size_t)S * F, 0);
-    p->ev_rec.clear();
+    if (p->profiling != 2) p->ev_rec.clear();   // mode 2 accumulates over runs
     // at most one run of overlap: run r-2's channel decoding must be done before
     // this run's demod reuses its ring slots
     const int par = (int)(p->run_idx & 1);
@@ -1275,7 +1275,11 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
 
 int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on) {
     if (!p) return fail(DABGPU_E_ARG, "null pipe");
-    p->profiling = on != 0;
+    if (on < 0 || on > 2) return fail(DABGPU_E_ARG, "profiling mode %d", on);
+    HIPCHK(hipStreamSynchronize(p->c->stream));         // events of earlier runs are complete
+    for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
+    p->profiling = on;
+    p->ev_rec.clear();
     return 0;
 }
 int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {

@@ -458,11 +458,14 @@ class Pipeline:
         pipeline's own stream, overlapping the next run's front end)"""
         _chk(lib().dabgpu_pipe_sync(self.h), "dabgpu_pipe_sync")
 
-    def set_profiling(self, on: bool = True) -> None:
-        _chk(lib().dabgpu_pipe_set_profiling(self.h, 1 if on else 0), "set_profiling")
+    def set_profiling(self, on=True) -> None:
+        """True/1: time the last run; 2: accumulate over every run from now on; False/0: off"""
+        mode = 0 if on is False else 1 if on is True else int(on)
+        _chk(lib().dabgpu_pipe_set_profiling(self.h, mode), "set_profiling")
 
     def timing(self) -> dict:
-        """per-stage kernel milliseconds and launch counts of the last run()"""
+        """per-stage kernel milliseconds and launch counts (last run, or summed since
+        set_profiling(2))"""
         ms = np.zeros(len(self.STAGES), np.float32)
         n = np.zeros(len(self.STAGES), np.int32)
         _chk(lib().dabgpu_pipe_timing(self.h, _p(ms), _p(n)), "timing")
