@@ -293,6 +293,44 @@ def test_pipeline_afc_tracks_oracle(ctx, cfo):
             assert fr.lp_window == info[gf].lp_window
 
 
+def test_pipeline_sample_drop_follows_oracle(ctx):
+    """Samples lost inside frame 4 shift every later frame by 300 samples: the
+    speculative front end (steady state: demod placed on the device by k_prs_sync's
+    startIndex) must find the shifted frames, cut its predictions after the first
+    mismatch and re-predict -- frame for frame the windows, startIndex values and NCO
+    phases of the sequential ofdmProcessor::run (oracle), and good FIBs around the
+    damaged frame."""
+    import dabamd
+    from dabamd.synth import Ensemble
+    subch = [(0, 96, 128, 3, 1, 0)]
+    F, runs = 3, 3
+    e = Ensemble(F * runs + 1, subch=subch, snr_db=40.0)
+    g = e.generate(17)
+    TF, TNULL, TU, TS = 196608, 2656, 2048, 2552
+    cut_at = g["frame0"] + 4 * TF + TNULL + TU + 60 * TS      # inside symbol 60 of frame 4
+    iq = g["iq"].reshape(-1, 2)
+    iq = np.ascontiguousarray(np.concatenate([iq[:cut_at], iq[cut_at + 300:]]).reshape(-1))
+    n = iq.size // 2
+    n_or, info, _ = orc.ofdm_run(iq, F * runs)
+    assert n_or == F * runs
+    diq = ctx.put(iq)
+    pipe = dabamd.Pipeline(ctx, 1, F, [dabamd.Subch(*subch[0][:4], 0, 0)])
+    pipe.acquire(diq, n, [0], [n])
+    for r in range(runs):
+        fic, crc, msc, valid = pipe.run(diq, n, [n])
+        frames, si = pipe.frames()
+        for f in range(F):
+            gf = r * F + f
+            assert frames[f].window == info[gf].window_start, (gf, frames[f].window, info[gf].window_start)
+            assert si[0, f] == info[gf].start_index, (gf, si[0, f], info[gf].start_index)
+            assert frames[f].lp_window == info[gf].lp_window, gf
+            if gf != 4:
+                assert crc[0, f].all(), gf
+    assert any(info[k].start_index != info[3].start_index for k in range(5, F * runs))   # the shift was seen
+    pipe.close()
+    diq.free()
+
+
 def test_pipeline_large_cfo_runs(ctx):
     """at 2.3 kHz the reference's coarse AFC wanders (startIndex up to ~1900): the pipeline
     must follow or stop cleanly, never read outside the stream"""
