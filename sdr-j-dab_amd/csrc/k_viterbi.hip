@@ -214,6 +214,22 @@ __device__ __forceinline__ uint32_t idx4(const ProfR &P, int t, int (&idx)[4]) {
     return k4;
 }
 
+// idx4 when every lane of the tile lies in one depuncturing segment (the common case:
+// segments span hundreds of steps): the segment's block start, input base and PI mask
+// arrive wave-uniform instead of through per-lane selects
+__device__ __forceinline__ uint32_t idx4_seg(int t, int bs, int ib, uint32_t m, int (&idx)[4]) {
+    const int p = 4 * t, blk = p >> 7;
+    const int n1 = __popc(m), oo = p & 127, b = oo & 31;
+    const int base = ib + (blk - bs) * 4 * n1 + (oo >> 5) * n1;
+    const uint32_t k4 = (m >> b) & 0xFu;
+    int i = base + __popc(m & ((1u << b) - 1u));
+#pragma unroll
+    for (int e = 0; e < 4; e++) {
+        idx[e] = i;
+        i += (k4 >> e) & 1;
+    }
+    return k4;
+}
 // the 4 soft values of one step of one codeword into half H of s[] (erasures and
 // steps past the codeword's end read as 0)
 template <int KIND, int H>
@@ -432,11 +448,32 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     // inputs of the next tile are loaded while the current one runs its ACS;
     // lane < VT handles step t0 + lane
     u16x2 s[NP][4];                                      // packed {A, B} soft values, per pair
-    auto fetch = [&](int t) {
+    // the depuncturing segments of profile 0 as plain scalars; the segment of a tile
+    // is a sum of boundary flags
+    // tb: first step of the tile (wave-uniform); t: this lane's step
+    auto fetch = [&](int tb, int t) {
         int i0[4];
         uint32_t k0 = 0;
-        if (t < stp[0] || (same && t < steps)) k0 = idx4(p0, t, i0);
-        else i0[0] = i0[1] = i0[2] = i0[3] = 0;
+        // one depuncturing segment for the whole tile (wave-uniform, scalar): the
+        // segment search of idx4 on the tile's first and last blocks
+        const int blo = (4 * tb) >> 7, bhi = (4 * (tb + VT - 1) + 3) >> 7;
+        int bs = 0, bs_hi = 0, ib = p0.in_base[0];
+        uint32_t m = p0.mask[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++) {
+            if (k < p0.nseg && blo >= p0.blk_end[k - 1]) { bs = p0.blk_end[k - 1]; ib = p0.in_base[k]; m = p0.mask[k]; }
+            if (k < p0.nseg && bhi >= p0.blk_end[k - 1]) bs_hi = p0.blk_end[k - 1];
+        }
+        const bool useg = p0.nseg > 0 && bhi < p0.last_end && bs == bs_hi;
+        if (t < stp[0] || (same && t < steps)) {
+            if (useg) {
+                k0 = idx4_seg(t, bs, ib, m, i0);
+            } else {
+                k0 = idx4(p0, t, i0);
+            }
+        } else {
+            i0[0] = i0[1] = i0[2] = i0[3] = 0;
+        }
         sfor<0, 2 * NP>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             int ik[4];
@@ -458,11 +495,11 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         for (int p = 0; p < NP; p++) put_bm(bm + p * 8 * BRS, lane, s[p]);
     };
     const bool mine = lane < VT;                         // lanes that build a step of the table
-    fetch(mine ? lane : steps);
+    fetch(0, mine ? lane : steps);
     for (int t0 = 0; t0 < steps; t0 += VT) {
         if (mine) put();
         wave_sync();
-        fetch(mine ? t0 + VT + lane : steps);
+        fetch(t0 + VT, mine ? t0 + VT + lane : steps);
         for (int u = 0; u < 2; u++) {
             const int tw = t0 + u * WS;
             if (tw >= steps) break;
