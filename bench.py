@@ -30,6 +30,7 @@ C3_SUBCH = [(96 * i, 96, 128, 3, 1, 0) for i in range(9)]   # (startAddr, CUs, k
 # C5: 16 ensembles x 16 DAB+ subchannels (64 kbit/s EEP-3A, 48 CUs, RSDims 8) = 256
 C5_SUBCH = [(48 * i, 48, 64, 0o103, 0, 1) for i in range(16)]
 WORKLOADS = {
+    "c2": ([], 64, "C2 at scale: 64 concurrent Mode-I ensembles/GPU, full frames (76 FFT'd symbols), FIC decode only"),
     "c3": (C3_SUBCH, 64, "C3: 64 concurrent Mode-I ensembles/GPU, FIC + full MSC (9 x UEP-3 128 kbps)"),
     "c5": (C5_SUBCH, 16, "C5: 256 DAB+ subchannels/GPU (16 ensembles x 16 x 64 kbps EEP-3A), FIC + MSC Viterbi "
                          "+ superframe sync + RS(120,110) + AU CRC"),
@@ -256,12 +257,14 @@ def main():
     dom = max(tm, key=lambda k: tm[k][0])
     # the pipeline decodes the FIC in the MSC's ACS launch (dabgpu.h, DABGPU_STAGE_FIC)
     acs_steps = E * 4 * F * sum(24 * s[2] + 6 for s in SUBCH) + E * F * 4 * (768 + 6)
-    acs_ms = tm["msc_acs"][1]                       # average launch duration
+    # (without MSC subchannels the FIC has launches of its own, k_acs<2>)
+    acs_stage, acs_kernel = ("msc_acs", "dab::k_acs2<3, 2>") if SUBCH else ("fic", "dab::k_acs<2>")
+    acs_ms = max(tm[acs_stage][1], 1e-9)            # average launch duration
     acs_ops = acs_steps * 64 * 4                    # 2 adds + compare + select per ACS
-    demod_ms = tm["demod"][1]
+    demod_ms = max(tm["demod"][1], 1e-9)
     demod_bytes = E * F * 75 * (8 * 2552 + 2 * 3072)
-    roof_valu = {"kernel": "k_acs2 (MSC + FIC Viterbi ACS)", "bound": "valu", "achieved": acs_ops / (acs_ms * 1e-3) / 1e12,
-                 "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "traffic": pmc_traffic("dab::k_acs2<3, 2>", args.workload),
+    roof_valu = {"kernel": f"{acs_kernel[5:]} (Viterbi ACS)", "bound": "valu", "achieved": acs_ops / (acs_ms * 1e-3) / 1e12,
+                 "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "traffic": pmc_traffic(acs_kernel, args.workload),
                  "note": "4 int ops per add-compare-select x 64 states per trellis step; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
     roof_valu["frac"] = roof_valu["achieved"] / roof_valu["peak"]
     roof_hbm = {"kernel": "k_demod_wg (FFT+DQPSK)", "bound": "hbm",

@@ -107,8 +107,9 @@ __device__ __forceinline__ float2 mix1(float2 v, const float2 *__restrict__ osc,
 }
 
 struct DemodTw {
-    float2 w1[7];                 // W2048^(t k), k = 1..7 (registers: used by every symbol)
-    const float2 *w256;           // LDS table W256^j: pass 2 W256^(t' k), pass 3 W32^(t'' k) = W256^(8 t'' k)
+    const float2 *w1;             // LDS table W2048^(t k) at [(k - 1) * 256 + t], k = 1..7
+    const float2 *w2;             // LDS table W256^(t' k) at [(k - 1) * 32 + t']: consecutive lanes, no bank conflicts
+    const float2 *w3;             // LDS table W32^(t'' k) at [(k - 1) * 4 + t'']: a quad's 4 values in 4 different banks
     float sg2, sg1;               // quad butterfly signs (+1 lower lane, -1 upper)
     bool rot;                     // lane t'' == 3 multiplies by -j between the two stages
 };
@@ -118,7 +119,7 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
     // pass 1
     dft8(a);
 #pragma unroll
-    for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w1[k - 1]);
+    for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w1[(k - 1) * DT + t]);
 #pragma unroll
     for (int k = 0; k < 8; k++) ex[k * 256 + t] = a[k];
     __syncthreads();
@@ -129,7 +130,7 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
     __syncthreads();
     dft8(a);
 #pragma unroll
-    for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w256[(tp * k) & 255]);
+    for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w2[(k - 1) * 32 + tp]);
 #pragma unroll
     for (int k = 0; k < 8; k++) ex[(k1 * 8 + k) * ZROW + tp] = a[k];
     __syncthreads();
@@ -140,7 +141,7 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
     dft8(a);
     if (tq) {                                      // t'' = 0: all twiddles 1
 #pragma unroll
-        for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w256[(8 * tq * k) & 255]);
+        for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w3[(k - 1) * 4 + tq]);
     }
     // pass 4: radix-4 over the quad's t''; lane t'' ends with K'' = brev2(t'')
 #pragma unroll
@@ -160,9 +161,16 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
     __shared__ int16_t st[2 * K + 2 * DT];
     __shared__ float2 fcw[DT / 64];
-    __shared__ float2 w256[256];
+    // twiddles, laid out per pass so that a wave's reads are conflict-free (the values
+    // are the W2048 table's entries: W256^j = W2048^(8 j), W32^j = W2048^(64 j))
+    __shared__ float2 w1s[7 * DT];      // pass 1: LDS instead of 14 VGPRs (room for the guard prefetch)
+    __shared__ float2 w2s[7 * 32];
+    __shared__ float2 w3s[7 * 4];
     const int t = threadIdx.x;
-    w256[t] = T.w2048[8 * t];
+#pragma unroll
+    for (int k = 1; k < 8; k++) w1s[(k - 1) * DT + t] = T.w2048[(t * k) & 2047];
+    if (t < 7 * 32) w2s[t] = T.w2048[(8 * ((t & 31) * (t / 32 + 1))) & 2047];
+    if (t < 7 * 4) w3s[t] = T.w2048[(64 * ((t & 3) * (t / 4 + 1))) & 2047];
     __syncthreads();
     const int item = blockIdx.x;
     const int fi = item / nchunks, ch = item % nchunks;
@@ -196,9 +204,9 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         DemodTw tw;
         {
             const int tq = t & 3;
-            tw.w256 = w256;
-#pragma unroll
-            for (int k = 1; k < 8; k++) tw.w1[k - 1] = T.w2048[(t * k) & 2047];
+            tw.w2 = w2s;
+            tw.w3 = w3s;
+            tw.w1 = w1s;
             tw.sg2 = (tq & 2) ? -1.0f : 1.0f;
             tw.sg1 = (tq & 1) ? -1.0f : 1.0f;
             tw.rot = tq == 3;
@@ -213,7 +221,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 cb[k3 >> 1] = (uint32_t)(uint16_t)T.carrier_of_bin[k1 + 8 * k2 + 64 * k3 + 512 * kk] |
                               ((uint32_t)(uint16_t)T.carrier_of_bin[k1 + 8 * k2 + 64 * (k3 + 1) + 512 * kk] << 16);
         }
-        float2 a[8], nx[8], P[8];
+        float2 a[8], nx[8], P[8], ng6, ng7;
         // warm-up symbol l0 - 1 (the PRS for the first chunk)
         {
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
@@ -224,6 +232,8 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         }
         {
             const int64_t u = fr.block0 + (int64_t)l0 * TS;
+            ng6 = s[u - 512 + t];
+            ng7 = s[u - 256 + t];
 #pragma unroll
             for (int m = 0; m < 8; m++) nx[m] = s[u + t + 256 * m];
         }
@@ -232,13 +242,17 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         for (int k = 0; k < 8; k++) P[k] = a[k];
         for (int l = l0; l < l1; l++) {
             const int64_t u0 = fr.block0 + (int64_t)l * TS;
-            // this symbol's samples (loaded one symbol ahead) and its guard samples
+            // this symbol's samples and its guard samples, all loaded one symbol ahead
+            // (a guard load issued here would expose a full HBM latency per symbol)
 #pragma unroll
             for (int m = 0; m < 8; m++) a[m] = nx[m];
-            float2 g6 = s[u0 - 512 + t], g7 = s[u0 - 256 + t];
+            float2 g6 = ng6, g7 = ng7;
             if (l + 1 < l1) {
+                const int64_t u1 = u0 + TS;
+                ng6 = s[u1 - 512 + t];
+                ng7 = s[u1 - 256 + t];
 #pragma unroll
-                for (int m = 0; m < 8; m++) nx[m] = s[u0 + TS + t + 256 * m];
+                for (int m = 0; m < 8; m++) nx[m] = s[u1 + t + 256 * m];
             }
             mix<GEN>(a, T.osc, fr.lp_data, fr.phase_b, u0 + t, dorg);
             g6 = mix1<GEN>(g6, T.osc, fr.lp_data, fr.phase_b, u0 - 512 + t, dorg);
