@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DABGPU_ABI_VERSION 1
+#define DABGPU_ABI_VERSION 2
 
 /* error codes */
 #define DABGPU_OK          0
@@ -101,6 +101,22 @@ typedef struct {
     int32_t flags;      /* bit0: run coarse AFC (f2Correction) in block0 */
 } dabgpu_frame;
 
+/* ---- host-side tables (no device needed; for pinning against the reference) --
+ *   DABGPU_TABLE_PRS     float2[2048] refTable (phasereference.cpp:40-47), natural order
+ *   DABGPU_TABLE_MAPPER  int16[1536]  permVector::mapIn (mapper.cpp:33-117)
+ *   DABGPU_TABLE_REFARG  float[18]    refArg (ofdm-decoder.cpp:71-74) */
+#define DABGPU_TABLE_PRS    1
+#define DABGPU_TABLE_MAPPER 2
+#define DABGPU_TABLE_REFARG 3
+int dabgpu_host_table(int which, void *out_h, size_t bytes);
+/* The depuncturing profile the decoder uses for a subchannel (deconvolve.cpp:142-366;
+ * uep_deconvolve's unknown-profile fallback to table row 1, :148-151): decoded bits,
+ * fragment size consumed, and the non-empty (L_i blocks of 128, PI_i) segments in
+ * order.  Returns 0, 1 when the UEP (bitRate, level) is not in the table (fallback),
+ * DABGPU_E_UNSUP when the protection is undefined. */
+int dabgpu_subch_profile(const dabgpu_subch *s, int32_t *nbits, int32_t *frag_size, int32_t *nseg,
+                         int32_t *L /*[4]*/, int32_t *PI /*[4]*/);
+
 /* ---- context ---------------------------------------------------------- */
 int         dabgpu_abi_version(void);
 const char *dabgpu_last_error(void);
@@ -141,10 +157,12 @@ int dabgpu_iq_convert(dabgpu_ctx *ctx, int format, const void *src_d, int64_t n_
 int dabgpu_prs_sync(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n,
                     int16_t level, int32_t *start_index_d, float *maxv_d, float *sumv_d);
 
-/* ofdmDecoder::processBlock_0 batched (ofdm-decoder.cpp:85-127, freqSyncMethod 1):
- * FFT of block 0; when frames[i].flags&1 the coarse offset estimate, else 0. */
-int dabgpu_block0(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n,
-                  int16_t *correction_d);
+/* ofdmDecoder::processBlock_0 batched (ofdm-decoder.cpp:85-162): FFT of block 0,
+ * snr_d[i] (optional) = get_snr (ofdm-decoder.cpp:212-230), and when
+ * frames[i].flags&1 the coarse offset estimate of freqSyncMethod `method`
+ * (0 getMiddle, 1 phase-difference correlation, 2 pattern match), else 0. */
+int dabgpu_block0(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n, int method,
+                  int16_t *correction_d, int16_t *snr_d);
 
 /* ofdmDecoder::processToken for symbols 1..75 of n frames (ofdm-decoder.cpp:167-190):
  * FFT, x conj(previous symbol), frequency de-interleave (mapper.cpp:115),
@@ -199,7 +217,9 @@ typedef struct {
     int32_t n_frames;          /* frames per dabgpu_pipe_run call */
     int32_t n_subch;
     int16_t threshold;         /* findIndex level (gui.cpp:98-99, default 3) */
-    int16_t freq_sync_method;  /* only 1 (main.cpp:91 default) is implemented */
+    int16_t freq_sync_method;  /* processBlock_0's coarse AFC: 0 getMiddle, 1 phase-difference
+                                  correlation (main.cpp:91 default), 2 pattern match
+                                  (ofdm-decoder.cpp:103-161) */
     const dabgpu_subch *subch;
 } dabgpu_pipe_cfg;
 
@@ -213,22 +233,48 @@ typedef struct {
     int32_t synced;
     int64_t cif_count;         /* CIFs delivered to the MSC so far */
     int32_t last_start_index;
-    int32_t resyncs;
+    int32_t resyncs;           /* sync losses (findIndex failed: goto notSynced, ofdm-processor.cpp:354-357) */
+    int32_t acquisitions;      /* null-symbol searches completed (SyncOnNull..SyncOnEndNull) */
+    int32_t attempts;          /* the reference's `attempts` counter (ofdm-processor.cpp:274-314) */
+    int32_t no_signal;         /* No_Signal_Found emissions (scan mode, > 5 failed attempts) */
+    int32_t frames_run;        /* frames this stream committed in the last dabgpu_pipe_run */
+    int32_t reserved;
 } dabgpu_stream_state;
+
+/* Per-frame record of the last run (the observables ofdmProcessor / ofdmDecoder
+ * report to the GUI, ofdm-processor.cpp:172-175,344-446, ofdm-decoder.cpp:93-97). */
+typedef struct {
+    int64_t window;            /* first sample of the frame's T_u sync window */
+    int32_t start_index;       /* findIndex result */
+    int32_t coarse;            /* coarseCorrector used for symbols 1..75 */
+    int16_t fine;              /* fineCorrector used for symbols 1..75 */
+    int16_t correction;        /* processBlock_0's return (0 when f2Correction was off) */
+    int16_t snr;               /* get_snr of block 0 (ofdm-decoder.cpp:212-230), before the IIR */
+    int16_t committed;         /* 1: the frame was decoded in this run */
+} dabgpu_frame_info;
 
 int dabgpu_pipe_create(dabgpu_ctx *ctx, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **out);
 int dabgpu_pipe_destroy(dabgpu_pipe *p);
 /* Acquire (notSynced/SyncOnNull/SyncOnEndNull, ofdm-processor.cpp:274-338)
- * every stream from sample start_h[s] of its IQ (device, stream s at iq_d +
- * 2*stream_stride*s, n_avail_h[s] samples). */
+ * every stream not yet synchronised from sample start_h[s] of its IQ (device,
+ * stream s at iq_d + 2*stream_stride*s, n_avail_h[s] samples).  Optional:
+ * dabgpu_pipe_run acquires unsynchronised streams itself, from their current
+ * position (sample 0 for a new pipeline). */
 int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride,
                         const int64_t *start_h, const int64_t *n_avail_h);
-/* Decode the next n_frames frames of every stream.  Outputs (device):
+/* Decode the next n_frames frames of every stream, as ofdmProcessor::run does:
+ * a stream whose findIndex fails goes back to the null-symbol search from where it
+ * is (goto notSynced, ofdm-processor.cpp:354-357) and continues with the frames
+ * after it.  Outputs (device):
  *   fic_bits_d  [n_streams][n_frames][4][768], fic_crc_d [n_streams][n_frames][12]
+ *               (frame f of stream s: its f-th frame of this run; frames past
+ *               dabgpu_stream_state.frames_run have CRC flags 0)
  *   msc_bits_d  [n_streams][4*n_frames][n_subch][msc_stride] (24*bitRate used)
- *   msc_valid_h [n_streams][4*n_frames] (host, optional): 1 where the CIF is
- *               past the 16-CIF warm-up.
- * Returns 0, or DABGPU_E_STATE if a stream lost sync (see dabgpu_pipe_state). */
+ *   msc_valid_h [n_streams][4*n_frames] (host, optional): 1 where the stream
+ *               delivered the CIF and it is past the 16-CIF warm-up.
+ * Returns 0 when every stream decoded n_frames frames, DABGPU_E_STATE when one
+ * ran out of samples (its decoded frames are still delivered; see
+ * dabgpu_pipe_state). */
 int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, const int64_t *n_avail_h,
                     uint8_t *fic_bits_d, uint8_t *fic_crc_d, uint8_t *msc_bits_d, int32_t msc_stride,
                     uint8_t *msc_valid_h);
@@ -242,6 +288,22 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, co
  *   info_d     [n_streams][4*n_frames][n_dabplus] */
 int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes_d, int32_t sf_stride, dabgpu_superframe *info_d);
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
+/* [n_streams][n_frames] records of the last dabgpu_pipe_run */
+int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info_h);
+/* ofdmProcessor's control methods, for one stream (stream = -1: every stream):
+ *   DABGPU_CTL_RESET        reset(): fine = coarse = 0, f2Correction on (ofdm-processor.cpp:476-479)
+ *   DABGPU_CTL_COARSE_ON    coarseCorrectorOn(): f2Correction on, coarse = 0 (:498-501)
+ *   DABGPU_CTL_COARSE_OFF   coarseCorrectorOff() (:503-505)
+ *   DABGPU_CTL_SCAN_ON/OFF  set_scanMode(bool) (:507-509): count No_Signal_Found
+ *   DABGPU_CTL_RESYNC       drop sync: the next run searches the null symbol again from
+ *                           the stream's current position (goto notSynced) */
+#define DABGPU_CTL_RESET      1
+#define DABGPU_CTL_COARSE_ON  2
+#define DABGPU_CTL_COARSE_OFF 3
+#define DABGPU_CTL_SCAN_ON    4
+#define DABGPU_CTL_SCAN_OFF   5
+#define DABGPU_CTL_RESYNC     6
+int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op);
 /* Wait until everything the pipeline enqueued is done.  The FIC/MSC/DAB+ outputs
  * of run r are written by back-end stream r & 1 (overlapping run r+1's OFDM front
  * end and channel decoding): call this before reading them, and give run r+1

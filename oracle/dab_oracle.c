@@ -294,6 +294,19 @@ static int16_t get_middle(const float *X) {  /* ofdm-decoder.cpp:233-258 (incl. 
     return (int16_t)(maxIndex - (ORC_TU - 1536) / 2);
 }
 
+/* get_snr (ofdm-decoder.cpp:212-230) of a T_u spectrum, sums in bin order as the
+ * reference; get_db(x) = 20 log10((x + 1) / 256) in float (dab-constants.h:107-109) */
+static float get_db(float x) { return 20 * log10f((x + 1) / (float)256); }
+int16_t orc_get_snr(const float *X) {
+    const int low = ORC_TU / 2 - ORC_K / 2, high = low + ORC_K;
+    float noise = 0, signal = 0;
+    for (int i = 10; i < low - 20; i++) { cf z = {X[2 * ((ORC_TU / 2 + i) % ORC_TU)], X[2 * ((ORC_TU / 2 + i) % ORC_TU) + 1]}; noise += cabs_f(z); }
+    for (int i = high + 20; i < ORC_TU - 10; i++) { cf z = {X[2 * ((ORC_TU / 2 + i) % ORC_TU)], X[2 * ((ORC_TU / 2 + i) % ORC_TU) + 1]}; noise += cabs_f(z); }
+    noise /= (low - 30 + ORC_TU - high - 30);
+    for (int i = ORC_TU / 2 - ORC_K / 4; i < ORC_TU / 2 + ORC_K / 4; i++) { cf z = {X[2 * ((ORC_TU / 2 + i) % ORC_TU)], X[2 * ((ORC_TU / 2 + i) % ORC_TU) + 1]}; signal += cabs_f(z); }
+    return (int16_t)(get_db(signal / (ORC_K / 2)) - get_db(noise));
+}
+
 static inline float arg_pair(const float *X, int a, int b) {
     cf x = {X[2 * (a % ORC_TU)], X[2 * (a % ORC_TU) + 1]}, y = {X[2 * (b % ORC_TU)], X[2 * (b % ORC_TU) + 1]};
     return carg_f(cmul_conjf(x, y));
@@ -394,13 +407,24 @@ static int get_samples(orc_src *s, cf *v, int n, int32_t phase) {  /* ofdm-proce
     return 1;
 }
 
+static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
+                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf);
 int orc_ofdm_run(const float *iq, int64_t n, int16_t threshold, int method,
                  int max_frames, orc_frame_info *info, int16_t *softbits) {
+    /* per call (reentrant: tests run the oracle on several streams from threads) */
+    float *envBuffer = (float *)malloc(sizeof(float) * 32768);
+    cf *buf = (cf *)malloc(sizeof(cf) * ORC_L * ORC_TS);
+    int ret = orc_ofdm_run_(iq, n, threshold, method, max_frames, info, softbits, envBuffer, buf);
+    free(envBuffer);
+    free(buf);
+    return ret;
+}
+
+static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
+                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf) {
     tables_init();
     orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0};
-    static float envBuffer[32768];
     const int mask = 32768 - 1;
-    cf buf[ORC_L * ORC_TS];
     float phase_ref[2 * ORC_TU];
     int16_t fine = 0; int32_t coarse = 0; int f2 = 1;
     int16_t prev1 = 1000, prev2 = 999;
@@ -490,8 +514,8 @@ notSynced:
 static int parity8(int x) { x ^= x >> 4; x ^= x >> 2; x ^= x >> 1; return x & 1; }
 
 /* k = 7, rate 1/4, polynomials {0155, 0117, 0123, 0155} (viterbi.cpp:62-63).
- * Soft input x in [-127,127] (punctured = 0) becomes sym = clamp(x+127,0,255)
- * (viterbi.cpp:229-235).  Branch metric sum_j sym_j ^ B_j with B in {0,255}
+ * Soft input x in [-127,127] (punctured = 0) becomes sym = clamp((int16_t)(x+127),0,255)
+ * (viterbi.cpp:229-235). Branch metric sum_j sym_j ^ B_j with B in {0,255}
  * (viterbi.cpp:159-164); ACS as FULL_SPIRAL (spiral-no-sse.c:193-223):
  * uint32 metrics, no renormalisation, strict ">" picks the upper
  * predecessor; start metrics 63 except state 0 = 0 (viterbi.cpp:360-371);
@@ -510,7 +534,7 @@ void orc_viterbi(const int16_t *in, int nbits, uint8_t *out) {
     for (int s = 0; s < steps; s++) {
         uint32_t sym[4];
         for (int j = 0; j < 4; j++) {
-            int t = in[4 * s + j] + 127;
+            int16_t t = (int16_t)(in[4 * s + j] + 127);   /* int16_t temp: wraps above 32640 */
             if (t < 0) t = 0;
             if (t > 255) t = 255;
             sym[j] = (uint32_t)t;
@@ -891,4 +915,15 @@ int orc_mp4_add(orc_mp4 *m, const uint8_t *bits, uint8_t *out, int16_t *n_correc
     }
     m->blocks = 4;
     return 2;
+}
+
+/* build every lazily initialised table once (call before using the oracle from threads) */
+void orc_init(void) {
+    float x[2 * ORC_TU], y[2 * ORC_TU];
+    memset(x, 0, sizeof x);
+    tables_init();
+    orc_fft2048(x, y, 0);
+    gf_init();
+    uint8_t b[11] = {0};
+    (void)orc_firecode_check(b);
 }

@@ -35,6 +35,7 @@ extern "C" {
 #define ORC_INPUT_RATE   2048000
 
 /* ---- tables ---- */
+void    orc_init(void);          /* builds the lazily initialised tables (thread-safe use after) */
 void    orc_mapper(int16_t *perm /*[1536]*/);                  /* mapper.cpp:33-55,84-86 */
 void    orc_ref_table(float *ref /*[2*2048] cf32*/);          /* phasereference.cpp:40-47 */
 float   orc_get_phi(int32_t k);                                /* phasetable.cpp:261-274 */
@@ -50,6 +51,7 @@ void    orc_fft2048(const float *in /*cf32[2048]*/, float *out, int inverse); /*
 int32_t orc_find_index(const float *v /*cf32[T_u]*/, int16_t level, float *maxv, float *sumv); /* phasereference.cpp:60-88 */
 int16_t orc_process_block0(const float *v /*cf32[T_u]*/, float *phase_ref /*cf32[T_u] out*/,
                            int flag, int method);             /* ofdm-decoder.cpp:85-162 */
+int16_t orc_get_snr(const float *X /*cf32[T_u] spectrum*/);      /* ofdm-decoder.cpp:212-230 */
 void    orc_process_token(const float *v /*cf32[T_s]*/, float *phase_ref /*cf32[T_u] in/out*/,
                           int16_t *ibits /*[3072]*/, float *softf /*[3072] or NULL*/); /* ofdm-decoder.cpp:167-190 */
 void    orc_freqcorr(const float *v /*cf32[T_s]*/, double *acc_re, double *acc_im,

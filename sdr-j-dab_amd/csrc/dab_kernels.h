@@ -16,14 +16,19 @@ constexpr int INPUT_RATE = 2048000;
 // own float expressions, see dabgpu.cpp: make_tables)
 struct OfdmTables {
     const float2 *osc;      // oscillatorTable[2048000] (ofdm-processor.cpp:79-81)
-    const float2 *tw;       // twiddle bases [12][64]: rows a=0..7 W2048^{n2*a}, rows 8+b W2048^{n2*8b}
-    const float2 *ref_l;    // PRS refTable in FFT output lane layout [i][lane]
+    const float2 *ref;      // PRS refTable[2048] (phasereference.cpp:40-47), natural bin order
     const float *refarg;    // refArg[18] (ofdm-decoder.cpp:71-74)
     const float2 *w2048;    // W2048^j = e^{-2 pi i j/2048}, j < 2048 (double, rounded to float)
     const int16_t *carrier_of_bin;   // [2048] carrier index of an FFT bin (mapper.cpp), -1 if none
     int32_t *err;           // device error word: kernels OR in DABGPU_KERR_* bits
 };
-constexpr int FRAME_SI_ON_DEVICE = 2;   // dabgpu_frame.flags bit (pipeline-internal)
+// outputs of the front-end kernels besides the soft bits
+struct DemodAux {
+    int32_t *si;            // findIndex per frame (k_demod_wg<.., true>, k_prs_wg); null: frames give block0
+    float *maxv, *sumv;     // optional: findIndex's Max and sum |r|
+    int16_t *snr;           // optional: get_snr of block 0 per frame
+    int32_t level;          // findIndex threshold
+};
 constexpr int KERR_FRAME = 1;      // frame descriptor outside its stream / bad NCO phase
 constexpr int KERR_VITERBI = 2;    // Viterbi source outside its buffer
 
@@ -33,13 +38,15 @@ struct AcqJob {
     int64_t end;
     int32_t local_phase;
     int32_t phase;          // coarse + fine
+    int32_t attempts;       // ofdmProcessor::run's `attempts` carried in (ofdm-processor.cpp:274-314)
+    int32_t scan;           // scanMode: count No_Signal_Found after > 5 failed attempts
 };
 struct AcqResult {
     int64_t window;
     int32_t local_phase;
     int32_t status;
-    int32_t attempts;
-    int32_t pad;
+    int32_t attempts;       // `attempts` after the search
+    int32_t no_signal;      // No_Signal_Found emissions during the search
 };
 
 // ---- Viterbi ------------------------------------------------------------
@@ -83,9 +90,9 @@ struct VitJob {
     // SRC_FIC: codeword = 4*i + blk over slots[i]
     const int32_t *slots;
     // SRC_MSC: codeword = ((stream * ncif) + c) * nsub + sub
-    int32_t nsub, ncif, ring;      // subchannels, CIFs in this batch, ring frames
-    int64_t cif0;                   // global CIF index of the batch's first CIF (per stream, same for all)
-    int32_t first_slot;             // ring slot of the batch's first frame
+    int32_t nsub, ncif, ring;      // subchannels, CIF slots per stream in this batch, ring frames
+    const int64_t *cif0s;           // [stream] CIF index (count delivered so far) of the batch's first CIF
+    const int32_t *ncifs;           // [stream] CIFs of the batch the stream delivered (<= ncif)
     const int32_t *sub_start;       // startAddr*64 per subchannel (up to 55232: int32)
     // outputs
     uint32_t *dec;                  // decision words (dec_bytes(n_cw, max nbits) bytes)
@@ -106,7 +113,8 @@ struct DpState {
 struct DpJob {
     const uint8_t *msc;             // MSC bits of the run: [S][ncif][nsub][msc_stride]
     int32_t msc_stride, ncif, nsub, ndp, nstreams;
-    int64_t cif0;
+    const int64_t *cif0s;           // [stream] CIF index of the run's first CIF slot
+    const int32_t *ncifs;           // [stream] CIFs the stream delivered in the run
     const int32_t *dp_sub;          // [ndp] subchannel index of each DAB+ subchannel
     const int16_t *dp_br;           // [ndp] its bitRate
     uint8_t *ring;                  // [S][ndp][120*DP_MAX_RS] 5-CIF byte rings
@@ -121,12 +129,12 @@ struct DpJob {
 hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
                            int level, int32_t *si, float *mx, float *sm, bool general);
 hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
-                         int16_t *corr, bool general);
-// si (optional): per-frame startIndex from k_prs_sync, used by frames flagged
-// FRAME_SI_ON_DEVICE (block0 and lp_data derived on the device)
+                         int method, int16_t *corr, int16_t *snr, bool general);
+// aux.si non-null: every frame is placed by its own findIndex (block0 = window +
+// startIndex), reported through aux; else the descriptors' block0 / lp_data are used
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
-                        const int32_t *si = nullptr);
+                        const DemodAux &aux);
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
 hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
                           AcqResult *res);
@@ -135,7 +143,7 @@ hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
 hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
-hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib);
+hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib, const int32_t *slots = nullptr);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
 hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_t n_values, float *dst);
 hipError_t launch_rs(hipStream_t st, const uint8_t *in, int n, const uint8_t *tabs, uint8_t *out, int16_t *ret);

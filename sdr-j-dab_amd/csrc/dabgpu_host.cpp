@@ -40,7 +40,6 @@ namespace {
 
 constexpr int M = 2048000;
 
-int brev5h(int k) { return ((k & 1) << 4) | ((k & 2) << 2) | (k & 4) | ((k & 8) >> 2) | ((k & 16) >> 4); }
 
 // Mode-I phase reference rows (k_min, i, n), k_max = k_min + 31 (phasetable.cpp:115-166)
 const int16_t kPhi[48][3] = {
@@ -63,7 +62,7 @@ float get_phi(int k) {                                   // phasetable.cpp:261-2
 }
 
 struct HostTables {
-    std::vector<float2> osc, tw, ref_l;
+    std::vector<float2> osc;
     std::vector<uint32_t> prbs_words;
     std::vector<float2> w2048;
     std::vector<int16_t> carrier_bin;
@@ -75,17 +74,6 @@ struct HostTables {
         osc.resize(M);
         for (int i = 0; i < M; i++)          // ofdm-processor.cpp:79-81
             osc[i] = make_float2((float)cos(2.0 * M_PI * i / M), (float)sin(2.0 * M_PI * i / M));
-        tw.resize(12 * 64);
-        for (int n2 = 0; n2 < 64; n2++) {
-            for (int a = 0; a < 8; a++) {
-                double ph = -2.0 * M_PI * (double)(n2 * a) / 2048.0;
-                tw[a * 64 + n2] = make_float2((float)cos(ph), (float)sin(ph));
-            }
-            for (int b = 0; b < 4; b++) {
-                double ph = -2.0 * M_PI * (double)(n2 * 8 * b) / 2048.0;
-                tw[(8 + b) * 64 + n2] = make_float2((float)cos(ph), (float)sin(ph));
-            }
-        }
         ref.assign(2048, make_float2(0.0f, 0.0f));
         for (int i = 1; i <= 768; i++) {      // phasereference.cpp:42-47
             float phi = get_phi(i);
@@ -104,11 +92,6 @@ struct HostTables {
         }
         std::vector<int> carrier_of_bin(2048, -1);
         for (int c = 0; c < 1536; c++) { int k = perm[c]; carrier_of_bin[k < 0 ? k + 2048 : k] = c; }
-        ref_l.resize(32 * 64);
-        for (int lane = 0; lane < 64; lane++) {
-            int k1 = lane >> 1, r = lane & 1;
-            for (int i = 0; i < 32; i++) ref_l[i * 64 + lane] = ref[k1 + 32 * brev5h(i) + 1024 * r];
-        }
         carrier_bin.resize(2048);              // k_demod: carrier of each FFT bin
         for (int b = 0; b < 2048; b++) carrier_bin[b] = (int16_t)carrier_of_bin[b];
         w2048.resize(2048);                    // k_demod twiddles
@@ -273,7 +256,7 @@ struct dabgpu_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
     hipEvent_t ev[16] = {};
-    float2 *osc = nullptr, *tw = nullptr, *ref_l = nullptr;
+    float2 *osc = nullptr, *ref = nullptr;
     uint32_t *prbs = nullptr;
     float2 *w2048 = nullptr;
     int16_t *carrier_bin = nullptr;
@@ -299,7 +282,7 @@ static int scratch(dabgpu_ctx *c, int slot, size_t bytes, void **p) {
     *p = c->scratch[slot];
     return 0;
 }
-enum { SC_DEC = 0, SC_PROF = 1, SC_I32 = 2, SC_FRAMES = 3, SC_FC = 4, SC_MISC = 5 };
+enum { SC_DEC = 0, SC_PROF = 1, SC_I32 = 2, SC_FRAMES = 3, SC_FC = 4, SC_MISC = 5, SC_ACQ = 6 };
 
 // read (and clear) the device error word; call after a stream synchronisation
 static int kernel_errors(dabgpu_ctx *c) {
@@ -322,6 +305,41 @@ static int upload(dabgpu_ctx *c, T **dst, const std::vector<T> &v) {
 extern "C" {
 
 int dabgpu_abi_version(void) { return DABGPU_ABI_VERSION; }
+
+int dabgpu_host_table(int which, void *out, size_t bytes) {
+    const HostTables &t = host_tables();
+    const void *src = nullptr;
+    size_t n = 0;
+    switch (which) {
+    case DABGPU_TABLE_PRS: src = t.ref.data(); n = t.ref.size() * sizeof(float2); break;
+    case DABGPU_TABLE_MAPPER: src = t.perm.data(); n = t.perm.size() * sizeof(int16_t); break;
+    case DABGPU_TABLE_REFARG: src = t.refarg.data(); n = t.refarg.size() * sizeof(float); break;
+    default: return fail(DABGPU_E_ARG, "unknown table %d", which);
+    }
+    if (!out || bytes < n) return fail(DABGPU_E_ARG, "table %d needs %zu bytes", which, n);
+    memcpy(out, src, n);
+    return 0;
+}
+
+int dabgpu_subch_profile(const dabgpu_subch *s, int32_t *nbits, int32_t *frag, int32_t *nseg, int32_t *L, int32_t *PI) {
+    if (!s || !nbits || !frag || !nseg || !L || !PI) return fail(DABGPU_E_ARG, "null arg");
+    Profile p;
+    if (make_profile(*s, p)) return fail(DABGPU_E_UNSUP, "protection (uep=%d, level 0%o) undefined", s->uepFlag, s->protLevel);
+    bool fallback = false;
+    if (s->uepFlag == 0) {
+        fallback = true;
+        for (int i = 0; i < kNumUep; i++)
+            if (kUepProfiles[i][0] == s->bitRate && kUepProfiles[i][1] == s->protLevel) fallback = false;
+    }
+    *nbits = p.nbits;
+    *frag = p.frag;
+    *nseg = p.nseg;
+    for (int k = 0; k < 4; k++) {
+        L[k] = k < p.nseg ? p.blk_end[k] - (k ? p.blk_end[k - 1] : 0) : 0;
+        PI[k] = k < p.nseg ? __builtin_popcount(p.mask[k]) - 8 : 0;
+    }
+    return fallback ? 1 : 0;
+}
 const char *dabgpu_last_error(void) { return g_err.c_str(); }
 
 int dabgpu_device_count(void) {
@@ -353,7 +371,7 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     const HostTables &t = host_tables();
     int rc = 0;
-    if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->tw, t.tw)) || (rc = upload(c, &c->ref_l, t.ref_l)) ||
+    if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->ref, t.ref)) ||
         (rc = upload(c, &c->w2048, t.w2048)) || (rc = upload(c, &c->carrier_bin, t.carrier_bin)) ||
         (rc = upload(c, &c->prbs, t.prbs_words)) ||
         (rc = upload(c, &c->refarg, t.refarg)) || (rc = upload(c, &c->dptab, t.dptab))) {
@@ -361,8 +379,7 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
         return rc;
     }
     c->T.osc = c->osc;
-    c->T.tw = c->tw;
-    c->T.ref_l = c->ref_l;
+    c->T.ref = c->ref;
     c->T.w2048 = c->w2048;
     c->T.carrier_of_bin = c->carrier_bin;
     c->T.refarg = c->refarg;
@@ -380,7 +397,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void *p : {(void *)c->osc, (void *)c->tw, (void *)c->ref_l, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
+    for (void *p : {(void *)c->osc, (void *)c->ref, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
                     (void *)c->refarg, (void *)c->err, (void *)c->dptab})
         if (p) (void)hipFree(p);
     if (c->h_err) (void)hipHostFree(c->h_err);
@@ -456,9 +473,11 @@ int dabgpu_prs_sync(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int 
     HIPCHK(launch_prs_sync(c->stream, iq, fr, n, c->T, level, si, mx, sm, true));
     return 0;
 }
-int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t *corr) {
+int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int method, int16_t *corr,
+                  int16_t *snr) {
     if (!c || !iq || !fr || !corr || n < 0) return fail(DABGPU_E_ARG, "bad args");
-    HIPCHK(launch_block0(c->stream, iq, fr, n, c->T, corr, true));
+    if (method < 0 || method > 2) return fail(DABGPU_E_UNSUP, "freqSyncMethod %d", method);
+    HIPCHK(launch_block0(c->stream, iq, fr, n, c->T, method, corr, snr, true));
     return 0;
 }
 // symbols 1..75 of a frame are split over `chunks` workgroups of k_demod (each
@@ -477,14 +496,15 @@ static int num_cus() {
     }
     return cus;
 }
-static int demod_chunks(int n) {
+// extra: FFTs every chunk adds besides its warm-up symbol (2 when it runs findIndex)
+static int demod_chunks(int n, int extra = 0) {
     const int cus = num_cus();
     const int64_t slots = (int64_t)kDemodWgPerCu * cus;
     int best = 1;
     double best_cost = 1e30;
     for (int c : {1, 2, 3, 5, 15, 25}) {
         const int64_t items = (int64_t)n * c;
-        const double cost = (double)((items + slots - 1) / slots) * ((NSYM + c - 1) / c + 1);
+        const double cost = (double)((items + slots - 1) / slots) * ((NSYM + c - 1) / c + 1 + extra);
         if (cost < best_cost - 1e-9) { best_cost = cost; best = c; }
     }
     return best;
@@ -495,7 +515,8 @@ static int demod_impl(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, in
     const int kChunks = demod_chunks(n);
     int rc = scratch(c, SC_FC, sizeof(float2) * (size_t)n * kChunks, &part);
     if (rc) return rc;
-    HIPCHK(launch_demod(c->stream, iq, fr, n, kChunks, c->T, soft, softf, (float *)part, general));
+    DemodAux aux{};
+    HIPCHK(launch_demod(c->stream, iq, fr, n, kChunks, c->T, soft, softf, (float *)part, general, aux));
     if (fc) HIPCHK(launch_fc_reduce(c->stream, (const float *)part, kChunks, n, fc));
     return 0;
 }
@@ -656,12 +677,18 @@ struct StreamSt {
     int64_t frame_count = 0;
     int32_t last_si = 504;
     int32_t resyncs = 0;
+    int32_t attempts = 0;        // ofdmProcessor::run's `attempts` (ofdm-processor.cpp:274-314)
+    int32_t no_signal = 0;       // No_Signal_Found emissions (scan mode)
+    int32_t frames_run = 0;      // frames committed by the last dabgpu_pipe_run
+    int32_t acquisitions = 0;    // null-symbol searches completed
 };
 
 struct dabgpu_pipe {
     dabgpu_ctx *c = nullptr;
     int S = 0, F = 0, NSUB = 0, R = 0;
     int16_t threshold = 3;
+    int16_t method = 1;              // freqSyncMethod
+    bool scan = false;               // scanMode (No_Signal_Found after > 5 attempts)
     std::vector<dabgpu_subch> sub;
     std::vector<StreamSt> st;
     int16_t *ring = nullptr;         // [S][R][75][3072]
@@ -669,9 +696,11 @@ struct dabgpu_pipe {
     int32_t *substart_d = nullptr;   // [NSUB]
     dabgpu_frame *frames_d = nullptr;
     int32_t *si_d = nullptr;
-    int16_t *corr_d = nullptr;
+    int16_t *corr_d = nullptr, *snr_d = nullptr;
     float *fc_d = nullptr, *fcpart_d = nullptr;
     int32_t *slots_d = nullptr;
+    int64_t *cif0_d = nullptr;       // [2][S] per back-end stream: CIF index of each stream's first CIF slot
+    int32_t *ncif_d = nullptr;       // [2][S] CIFs each stream delivered in the run
     uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
     size_t dec_sz = 0;
     int64_t dec_fic_off = 0;                    // FIC decisions: words after the MSC's
@@ -681,9 +710,11 @@ struct dabgpu_pipe {
     dabgpu_frame *h_frames = nullptr;
     int32_t *h_si = nullptr;
     float2 *h_fc = nullptr;
+    int16_t *h_snr = nullptr;
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
     std::vector<int32_t> last_si;
+    std::vector<dabgpu_frame_info> last_info;   // [S][F] observables of the last run
     // DAB+ superframe layer (mp4Processor per DAB+ subchannel and stream)
     int NDP = 0, dp_max_rs = 0;
     int32_t *dp_sub_d = nullptr;
@@ -691,9 +722,8 @@ struct dabgpu_pipe {
     uint8_t *dp_ring_d = nullptr;     // [S][NDP][120*DP_MAX_RS]
     DpState *dp_state_d = nullptr;    // [S][NDP]
     uint8_t *dp_code_d = nullptr;     // [S][NDP][4F] superframe verdict per candidate CIF
-    const uint8_t *last_msc = nullptr; // MSC bits of the last successful run
+    const uint8_t *last_msc = nullptr; // MSC bits of the last run
     int32_t last_msc_stride = 0;
-    int64_t last_cif0 = 0;
     // channel decoding (FIC/MSC Viterbi, DAB+) of run r runs on back-end stream
     // vs[r & 1], so run r's back end overlaps run r+1's front end AND run r+1's back
     // end (whose first waves fill the SIMDs run r's last Viterbi waves leave idle).
@@ -754,7 +784,8 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     if (!c || !cfg || !out) return fail(DABGPU_E_ARG, "null arg");
     *out = nullptr;
     if (cfg->n_streams <= 0 || cfg->n_frames <= 0 || cfg->n_subch < 0) return fail(DABGPU_E_ARG, "bad sizes");
-    if (cfg->freq_sync_method != 1) return fail(DABGPU_E_UNSUP, "freqSyncMethod %d not implemented (only 1)", cfg->freq_sync_method);
+    if (cfg->freq_sync_method < 0 || cfg->freq_sync_method > 2)
+        return fail(DABGPU_E_UNSUP, "freqSyncMethod %d (0, 1 or 2: ofdm-decoder.cpp:103-161)", cfg->freq_sync_method);
     auto *p = new dabgpu_pipe();
     p->c = c;
     p->S = cfg->n_streams;
@@ -762,6 +793,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     p->NSUB = cfg->n_subch;
     p->R = 2 * cfg->n_frames + 4;
     p->threshold = cfg->threshold;
+    p->method = cfg->freq_sync_method;
     p->sub.assign(cfg->subch, cfg->subch + cfg->n_subch);
     p->st.assign(p->S, StreamSt());
     std::vector<Profile> profs(std::max(1, p->NSUB));
@@ -791,13 +823,17 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->frames_d, sizeof(dabgpu_frame) * SF);
     A((void **)&p->si_d, sizeof(int32_t) * SF);
     A((void **)&p->corr_d, sizeof(int16_t) * SF);
+    A((void **)&p->snr_d, sizeof(int16_t) * SF);
     A((void **)&p->fc_d, sizeof(float2) * SF);
     A((void **)&p->fcpart_d, sizeof(float2) * SF * kMaxChunks);
     if (!rc && (hipHostMalloc((void **)&p->h_frames, sizeof(dabgpu_frame) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_si, sizeof(int32_t) * SF, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&p->h_fc, sizeof(float2) * SF, hipHostMallocDefault) != hipSuccess))
+                hipHostMalloc((void **)&p->h_fc, sizeof(float2) * SF, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_snr, sizeof(int16_t) * SF, hipHostMallocDefault) != hipSuccess))
         rc = fail(DABGPU_E_NOMEM, "pipe pinned staging");
     A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
+    A((void **)&p->cif0_d, sizeof(int64_t) * p->S * 2);
+    A((void **)&p->ncif_d, sizeof(int32_t) * p->S * 2);
     // MSC decisions, then the FIC's (both jobs of one run decode in one launch)
     const int64_t msc_words = p->NSUB > 0 ? dec_bytes(SF * 4 * p->NSUB, p->max_nbits) / 4 : 0;
     p->dec_fic_off = msc_words;
@@ -869,51 +905,78 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
-    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc})
+    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr})
         if (h) (void)hipHostFree(h);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
-                    (void *)p->corr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
+                    (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
+                    (void *)p->cif0_d, (void *)p->ncif_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
 }
 
-int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *start_h, const int64_t *n_avail_h) {
-    if (!p || !iq || !start_h || !n_avail_h) return fail(DABGPU_E_ARG, "null arg");
+}  // extern "C"
+
+// Null-symbol search (notSynced .. SyncOnEndNull, ofdm-processor.cpp:274-338) for the
+// streams `who` of `cur`, each from its current position (window, localPhase) with
+// its correctors: one k_acquire wave per stream.  A stream that finds the end of a
+// null symbol is synchronised at SyncOnPhase; one that runs out of samples stays
+// unsynchronised at the end of its samples (the next call continues from there).
+static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
+                           const std::vector<int> &who, std::vector<StreamSt> &cur, int &found) {
     dabgpu_ctx *c = p->c;
+    found = 0;
+    if (who.empty()) return 0;
     std::vector<AcqJob> jobs;
-    std::vector<int> who;
-    for (int s = 0; s < p->S; s++) {
-        if (p->st[s].synced) continue;
+    for (int s : who) {
         AcqJob j;
+        memset(&j, 0, sizeof j);
         j.iq_base = stride * s;
-        j.start = start_h[s];
-        j.end = n_avail_h[s];
-        j.local_phase = p->st[s].lp;
-        j.phase = p->st[s].coarse + p->st[s].fine;
+        j.start = cur[s].window;
+        j.end = n_avail[s];
+        j.local_phase = cur[s].lp;
+        j.phase = cur[s].coarse + cur[s].fine;
+        j.attempts = cur[s].attempts;
+        j.scan = p->scan ? 1 : 0;
         jobs.push_back(j);
-        who.push_back(s);
     }
-    if (jobs.empty()) return 0;
     void *jd = nullptr, *rd = nullptr;
     int rc = scratch(c, SC_MISC, sizeof(AcqJob) * jobs.size(), &jd);
     if (rc) return rc;
-    if ((rc = scratch(c, SC_FC, sizeof(AcqResult) * jobs.size(), &rd))) return rc;
+    if ((rc = scratch(c, SC_ACQ, sizeof(AcqResult) * jobs.size(), &rd))) return rc;
     HIPCHK(hipMemcpyAsync(jd, jobs.data(), sizeof(AcqJob) * jobs.size(), hipMemcpyHostToDevice, c->stream));
     HIPCHK(launch_acquire(c->stream, iq, (const AcqJob *)jd, (int)jobs.size(), c->osc, (AcqResult *)rd));
     std::vector<AcqResult> res(jobs.size());
     HIPCHK(hipMemcpyAsync(res.data(), rd, sizeof(AcqResult) * jobs.size(), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    int bad = 0;
     for (size_t i = 0; i < jobs.size(); i++) {
-        StreamSt &S = p->st[who[i]];
+        StreamSt &S = cur[who[i]];
         S.lp = res[i].local_phase;
         S.window = res[i].window;
-        if (res[i].status == 0) S.synced = true;
-        else bad++;
+        S.attempts = res[i].attempts;
+        S.no_signal += res[i].no_signal;
+        if (res[i].status == 0) {
+            S.synced = true;
+            S.acquisitions++;
+            found++;
+        }
     }
-    if (bad) return fail(DABGPU_E_STATE, "%d stream(s) found no null symbol", bad);
+    return 0;
+}
+
+extern "C" int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *start_h,
+                                   const int64_t *n_avail_h) {
+    if (!p || !iq || !start_h || !n_avail_h) return fail(DABGPU_E_ARG, "null arg");
+    std::vector<int> who;
+    for (int s = 0; s < p->S; s++)
+        if (!p->st[s].synced) {
+            who.push_back(s);
+            p->st[s].window = start_h[s];
+        }
+    int found = 0;
+    if (int rc = acquire_streams(p, iq, stride, n_avail_h, who, p->st, found)) return rc;
+    if (found < (int)who.size()) return fail(DABGPU_E_STATE, "%d stream(s) found no null symbol", (int)who.size() - found);
     return 0;
 }
 
@@ -976,35 +1039,46 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     const int n = (int)fr.size();
     progress = false;
     if (n == 0) return 0;
-    // Steady state (no stream runs the coarse AFC of processBlock_0): the demod of
-    // every predicted frame follows k_prs_sync on the device, which places each frame
-    // at its measured startIndex -- one host round trip per pass instead of two.
-    // Frames the replay below does not commit are re-predicted and decoded again.
+    // Steady state (no stream runs the coarse AFC of processBlock_0): ONE launch per
+    // pass -- every predicted frame's workgroup runs findIndex on its window, places
+    // the frame at the startIndex it finds, reports get_snr of block 0 and demodulates
+    // the 75 symbols (k_demod_wg<.., SYNC>); one host round trip per pass.  Frames the
+    // replay below does not commit are re-predicted and decoded again.  While a
+    // stream's coarse AFC is pending the host needs startIndex and processBlock_0's
+    // correction first: findIndex, block 0 and the demod run as three launches.
     bool fast = true;
     for (const dabgpu_frame &d : fr) fast = fast && !(d.flags & 1);
-    if (fast)
-        for (dabgpu_frame &d : fr) d.flags |= FRAME_SI_ON_DEVICE;
     memcpy(p->h_frames, fr.data(), sizeof(dabgpu_frame) * n);
     HIPCHK(hipMemcpyAsync(p->frames_d, p->h_frames, sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
-    HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
-    HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
-    HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
     std::vector<int32_t> si(n);
     std::vector<float2> fc_all;
+    std::vector<int16_t> snr_all;
     if (fast) {
         fc_all.resize(n);
+        snr_all.resize(n);
+        DemodAux aux{};
+        aux.si = p->si_d;
+        aux.snr = p->snr_d;
+        aux.level = p->threshold;
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
-        const int kChunks = demod_chunks(n);
-        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general,
-                            p->si_d));
+        const int kChunks = demod_chunks(n, 2);
+        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n, p->fc_d));
         HIPCHK(hipMemcpyAsync(p->h_fc, p->fc_d, sizeof(float2) * n, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(p->h_snr, p->snr_d, sizeof(int16_t) * n, hipMemcpyDeviceToHost, c->stream));
+    } else {
+        HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
+        HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
+        HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
     }
     HIPCHK(hipMemcpyAsync(p->h_si, p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     if (int rc = kernel_errors(c)) return rc;
     memcpy(si.data(), p->h_si, sizeof(int32_t) * n);
-    if (fast) memcpy(fc_all.data(), p->h_fc, sizeof(float2) * n);
+    if (fast) {
+        memcpy(fc_all.data(), p->h_fc, sizeof(float2) * n);
+        memcpy(snr_all.data(), p->h_snr, sizeof(int16_t) * n);
+    }
     // pass 1: windows.  A frame is usable if every earlier frame of its stream
     // had the predicted startIndex; its own startIndex fixes block0.
     std::vector<char> ok(n, 0);
@@ -1031,22 +1105,24 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
             if (si[i] != pred_si[i]) { cut[i] = 1; valid = false; }
         }
     }
-    // pass 2: block 0 (coarse AFC) for the usable frames with f2 on
+    // pass 2: processBlock_0 (get_snr; coarse AFC for the frames with f2 on) of the
+    // usable frames -- in the steady state the fused demod did it already
     std::vector<int> idx;
     for (int i = 0; i < n; i++) if (ok[i]) idx.push_back(i);
     std::vector<dabgpu_frame> fr2;
     for (int i : idx) fr2.push_back(fr[i]);
     const int n2 = (int)fr2.size();
-    std::vector<int16_t> corr(n2, 0);
-    bool any_f2 = false;
-    for (auto &d : fr2) if (d.flags & 1) any_f2 = true;
-    if (n2 && any_f2) {
+    std::vector<int16_t> corr(n2, 0), snr2(n2, 0);
+    if (n2 && !fast) {
         HIPCHK(hipMemcpyAsync(p->frames_d, fr2.data(), sizeof(dabgpu_frame) * n2, hipMemcpyHostToDevice, c->stream));
         HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, true));
-        HIPCHK(launch_block0(c->stream, iq, p->frames_d, n2, c->T, p->corr_d, general));
+        HIPCHK(launch_block0(c->stream, iq, p->frames_d, n2, c->T, p->method, p->corr_d, p->snr_d, general));
         HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, false));
         HIPCHK(hipMemcpyAsync(corr.data(), p->corr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
+        HIPCHK(hipMemcpyAsync(snr2.data(), p->snr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
         if (int rc = kernel_errors(c)) return rc;
+    } else if (n2) {
+        for (int k = 0; k < n2; k++) snr2[k] = snr_all[idx[k]];
     }
     // replay the coarse corrector with the measured corrections; phase_b of a
     // frame uses its own correction, later frames are cut if the corrector moved
@@ -1076,8 +1152,11 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
             if (cut[i]) valid = false;
         }
     }
-    std::vector<int16_t> corr_i(n, 0);
-    for (int k = 0; k < n2; k++) corr_i[idx[k]] = corr[k];
+    std::vector<int16_t> corr_i(n, 0), snr_i(n, 0);
+    for (int k = 0; k < n2; k++) {
+        corr_i[idx[k]] = corr[k];
+        snr_i[idx[k]] = snr2[k];
+    }
     // pass 3: demod of the frames still usable
     std::vector<int> idx3;
     std::vector<dabgpu_frame> fr3;
@@ -1087,11 +1166,11 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     if (n3 && fast) {
         for (int k = 0; k < n3; k++) fc[k] = fc_all[idx3[k]];   // demodulated above
     } else if (n3) {
-        for (dabgpu_frame &d : fr3) d.flags &= ~FRAME_SI_ON_DEVICE;
         HIPCHK(hipMemcpyAsync(p->frames_d, fr3.data(), sizeof(dabgpu_frame) * n3, hipMemcpyHostToDevice, c->stream));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         const int kChunks = demod_chunks(n3);
-        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general));
+        DemodAux aux{};
+        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
         HIPCHK(hipMemcpyAsync(fc.data(), p->fc_d, sizeof(float2) * n3, hipMemcpyDeviceToHost, c->stream));
@@ -1132,6 +1211,16 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
             x.last_si = (int32_t)(d.block0 - d.window);
             p->last_frames[(size_t)s * p->F + done[s]] = d;
             p->last_si[(size_t)s * p->F + done[s]] = x.last_si;
+            {
+                dabgpu_frame_info &fi = p->last_info[(size_t)s * p->F + done[s]];
+                fi.window = d.window;
+                fi.start_index = x.last_si;
+                fi.coarse = coarse0;
+                fi.fine = fine0;
+                fi.correction = corr_i[i];
+                fi.snr = snr_i[i];
+                fi.committed = 1;
+            }
             done[s]++;
             x.frame_count++;
             progress = true;
@@ -1155,14 +1244,19 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     return 0;
 }
 
+extern "C" {
+
 int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail, uint8_t *fic_bits,
                     uint8_t *fic_crc, uint8_t *msc_bits, int32_t msc_stride, uint8_t *msc_valid) {
     if (!p || !iq || !n_avail) return fail(DABGPU_E_ARG, "null arg");
     dabgpu_ctx *c = p->c;
     const int S = p->S, F = p->F;
-    for (int s = 0; s < S; s++) if (!p->st[s].synced) return fail(DABGPU_E_STATE, "stream %d not synchronised", s);
+    const bool do_msc = msc_bits && p->NSUB > 0;
+    if (do_msc && msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
     p->last_frames.assign((size_t)S * F, dabgpu_frame());
     p->last_si.assign((size_t)S * F, 0);
+    p->last_info.assign((size_t)S * F, dabgpu_frame_info());
+    p->last_msc = nullptr;
     if (p->profiling != 2) p->ev_rec.clear();   // mode 2 accumulates over runs
     // at most one run of overlap: run r-2's channel decoding must be done before
     // this run's demod reuses its ring slots
@@ -1170,35 +1264,53 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     if (p->back_rec[par]) HIPCHK(hipStreamWaitEvent(c->stream, p->ev_back[par], 0));
     std::vector<int> done(S, 0);
     std::vector<StreamSt> cur = p->st;
-    bool lost = false;
-    for (int it = 0; it < 4 * F + 8; it++) {
-        bool progress = false;
-        int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost);
-        if (rc) return rc;
-        if (!progress) break;
+    // ofdmProcessor::run per stream: speculative front-end passes commit frames; a
+    // stream that loses sync (or was never synchronised) searches the next null
+    // symbol from where it is and continues (goto notSynced, ofdm-processor.cpp:354-357).
+    // Every pass either commits a frame or moves a stream past samples, so this ends.
+    for (int it = 0; it < 64 * F + 64; it++) {
+        std::vector<int> who;
+        for (int s = 0; s < S; s++)
+            if (!cur[s].synced && done[s] < F) who.push_back(s);
+        int found = 0;
+        if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) return rc;
+        bool progress = false, lost = false;
+        if (int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost)) return rc;
+        if (!progress && !lost && !found) break;
     }
     bool all = true;
-    for (int s = 0; s < S; s++) if (done[s] != F) all = false;
+    for (int s = 0; s < S; s++) {
+        if (done[s] != F) all = false;
+        cur[s].frames_run = done[s];
+    }
     // channel decoding on the pipeline's stream, after this run's front end
     p->cur = par;
     hipStream_t bs = p->vs[par];
     HIPCHK(hipEventRecord(p->ev_front, c->stream));
     HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
-    // FIC for every committed frame, MSC for all subchannels of all CIFs of this run.
+    // per stream: CIF index of its first CIF slot and the CIFs it delivered
+    {
+        std::vector<int64_t> c0(S);
+        std::vector<int32_t> nc(S);
+        for (int s = 0; s < S; s++) {
+            c0[s] = p->st[s].cif_count;
+            nc[s] = 4 * done[s];
+        }
+        HIPCHK(hipMemcpyAsync(p->cif0_d + (size_t)par * S, c0.data(), sizeof(int64_t) * S, hipMemcpyHostToDevice, bs));
+        HIPCHK(hipMemcpyAsync(p->ncif_d + (size_t)par * S, nc.data(), sizeof(int32_t) * S, hipMemcpyHostToDevice, bs));
+    }
+    // FIC for every committed frame, MSC for all subchannels of every delivered CIF.
     // With both, one ACS and one traceback launch decode them together (the FIC's short
     // waves fill the SIMDs the MSC's last waves leave idle); decisions in separate
     // halves of this stream's decision buffer.
-    const int64_t cif0 = p->st[0].cif_count;
-    const bool do_msc = msc_bits && p->NSUB > 0 && all;
-    if (do_msc && msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
     VitJob JF, JM;
     memset(&JF, 0, sizeof JF);
     memset(&JM, 0, sizeof JM);
+    int32_t *slots_d = p->slots_d + (size_t)par * S * F;
     if (fic_bits) {
         std::vector<int32_t> slots((size_t)S * F);
         for (int s = 0; s < S; s++)
-            for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = p->last_frames[(size_t)s * F + f].out_slot;
-        int32_t *slots_d = p->slots_d + (size_t)par * S * F;
+            for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = f < done[s] ? p->last_frames[(size_t)s * F + f].out_slot : -1;
         HIPCHK(hipMemcpyAsync(slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, bs));
         JF.kind = SRC_FIC;
         JF.n_cw = 4 * S * F;
@@ -1224,7 +1336,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         JM.nsub = p->NSUB;
         JM.ncif = 4 * F;
         JM.ring = p->R;
-        JM.cif0 = cif0;
+        JM.cif0s = p->cif0_d + (size_t)par * S;
+        JM.ncifs = p->ncif_d + (size_t)par * S;
         JM.sub_start = p->substart_d;
         JM.out = msc_bits;
         JM.out_stride = msc_stride;
@@ -1241,12 +1354,12 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F));
+        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, slots_d));
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
     } else if (fic_bits) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
         HIPCHK(launch_viterbi(bs, JF));
-        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F));
+        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, slots_d));
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
     } else if (do_msc) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
@@ -1259,17 +1372,15 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     HIPCHK(hipEventRecord(p->ev_back[par], bs));
     p->back_rec[par] = true;
     p->run_idx++;
-    p->last_msc = (msc_bits && p->NSUB > 0 && all) ? msc_bits : nullptr;
+    p->last_msc = do_msc ? msc_bits : nullptr;
     p->last_msc_stride = msc_stride;
-    p->last_cif0 = cif0;
     if (msc_valid)
         for (int s = 0; s < S; s++)
-            for (int q = 0; q < 4 * F; q++) msc_valid[(size_t)s * 4 * F + q] = (all && cif0 + q >= 16) ? 1 : 0;
-    for (int s = 0; s < S; s++) {
-        cur[s].cif_count = p->st[s].cif_count + 4 * (int64_t)done[s];
-    }
+            for (int q = 0; q < 4 * F; q++)
+                msc_valid[(size_t)s * 4 * F + q] = (q < 4 * done[s] && p->st[s].cif_count + q >= 16) ? 1 : 0;
+    for (int s = 0; s < S; s++) cur[s].cif_count = p->st[s].cif_count + 4 * (int64_t)done[s];
     p->st = cur;
-    if (lost || !all) return fail(DABGPU_E_STATE, "a stream lost sync or ran out of samples (see dabgpu_pipe_state)");
+    if (!all) return fail(DABGPU_E_STATE, "a stream ran out of samples (see dabgpu_pipe_state)");
     return 0;
 }
 
@@ -1311,7 +1422,7 @@ int dabgpu_pipe_sync(dabgpu_pipe *p) {
 int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, dabgpu_superframe *info) {
     if (!p || !sf_bytes || !info) return fail(DABGPU_E_ARG, "null arg");
     if (p->NDP == 0) return fail(DABGPU_E_STATE, "no DAB+ subchannel in this pipeline");
-    if (!p->last_msc) return fail(DABGPU_E_STATE, "no successful dabgpu_pipe_run with MSC output to consume");
+    if (!p->last_msc) return fail(DABGPU_E_STATE, "no dabgpu_pipe_run with MSC output to consume");
     if (sf_stride < 110 * p->dp_max_rs) return fail(DABGPU_E_ARG, "sf_stride %d < %d", sf_stride, 110 * p->dp_max_rs);
     dabgpu_ctx *c = p->c;
     DpJob J;
@@ -1322,7 +1433,8 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.nsub = p->NSUB;
     J.ndp = p->NDP;
     J.nstreams = p->S;
-    J.cif0 = p->last_cif0;
+    J.cif0s = p->cif0_d + (size_t)p->cur * p->S;
+    J.ncifs = p->ncif_d + (size_t)p->cur * p->S;
     J.dp_sub = p->dp_sub_d;
     J.dp_br = p->dp_br_d;
     J.ring = p->dp_ring_d;
@@ -1361,6 +1473,37 @@ int dabgpu_pipe_state(dabgpu_pipe *p, int s, dabgpu_stream_state *o) {
     o->cif_count = x.cif_count;
     o->last_start_index = x.last_si;
     o->resyncs = x.resyncs;
+    o->acquisitions = x.acquisitions;
+    o->attempts = x.attempts;
+    o->no_signal = x.no_signal;
+    o->frames_run = x.frames_run;
+    o->reserved = 0;
+    return 0;
+}
+
+int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info) {
+    if (!p || !info) return fail(DABGPU_E_ARG, "bad args");
+    if (p->last_info.empty()) memset(info, 0, sizeof(dabgpu_frame_info) * (size_t)p->S * p->F);
+    else memcpy(info, p->last_info.data(), sizeof(dabgpu_frame_info) * p->last_info.size());
+    return 0;
+}
+
+int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op) {
+    if (!p || stream < -1 || stream >= p->S) return fail(DABGPU_E_ARG, "bad args");
+    if (op == DABGPU_CTL_SCAN_ON || op == DABGPU_CTL_SCAN_OFF) {      // set_scanMode (one flag, like the reference's)
+        p->scan = op == DABGPU_CTL_SCAN_ON;
+        return 0;
+    }
+    for (int s = (stream < 0 ? 0 : stream); s < (stream < 0 ? p->S : stream + 1); s++) {
+        StreamSt &x = p->st[s];
+        switch (op) {
+        case DABGPU_CTL_RESET: x.fine = 0; x.coarse = 0; x.f2 = true; break;      // ofdm-processor.cpp:476-479
+        case DABGPU_CTL_COARSE_ON: x.f2 = true; x.coarse = 0; break;             // :498-501
+        case DABGPU_CTL_COARSE_OFF: x.f2 = false; break;                         // :503-505
+        case DABGPU_CTL_RESYNC: x.synced = false; break;
+        default: return fail(DABGPU_E_ARG, "unknown control op %d", op);
+        }
+    }
     return 0;
 }
 

@@ -245,8 +245,9 @@ __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     const int br = J.dp_br[dp], sub = J.dp_sub[dp];
     const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
     uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
-    // a window holding an undelivered CIF (de-interleaver warm-up) is never evaluated
-    if (J.cif0 + cl - 4 < 16) {
+    // a window holding an undelivered CIF (de-interleaver warm-up, or a CIF slot the
+    // stream did not fill in this run) is never evaluated
+    if (cl >= J.ncifs[stream] || J.cif0s[stream] + cl - 4 < 16) {
         if (lane == 0) *code = 0;
         return;
     }
@@ -389,6 +390,8 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
     const int br = J.dp_br[dp], sub = J.dp_sub[dp], nbytes = 3 * br;
     DpState st = J.state[sd];
     const uint8_t *code = J.code + (int64_t)sd * J.ncif;
+    const int nd = J.ncifs[stream];                     // CIFs this stream delivered
+    const int64_t cif0 = J.cif0s[stream];
     for (int c0 = 0; c0 < J.ncif; c0 += 64) {
         const int cl = c0 + lane;
         const int v = cl < J.ncif ? code[cl] : 0;
@@ -396,8 +399,8 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
         const int nc = min(64, J.ncif - c0);
         for (int i = 0; i < nc; i++) {                  // uniform
             int s;
-            if (J.cif0 + c0 + i < 16) {
-                s = -1;                                  // de-interleaver warm-up: nothing delivered
+            if (c0 + i >= nd || cif0 + c0 + i < 16) {
+                s = -1;                                  // not delivered (warm-up, or past the stream's CIFs)
             } else {
                 st.blocks++;
                 st.fill = (st.fill + 1) % 5;
@@ -421,11 +424,17 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
             J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
         }
     }
+    // carry = the stream's last 4 delivered CIFs (oldest first); with fewer than 4 new
+    // ones the older part comes from the previous carry (staged: it is overwritten)
+    __shared__ uint8_t nc[4 * 3 * 384];
     uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
     for (int p = lane; p < 4 * nbytes; p += 64) {
-        const int b = p / nbytes, w = p - b * nbytes, q = J.ncif - 4 + b;
-        carry[p] = (uint8_t)pack_byte(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride, w);
+        const int b = p / nbytes, w = p - b * nbytes, q = nd - 4 + b;
+        nc[p] = q >= 0 ? (uint8_t)pack_byte(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride, w)
+                       : carry[(q + 4) * nbytes + w];
     }
+    wave_sync();
+    for (int p = lane; p < 4 * nbytes; p += 64) carry[p] = nc[p];
     if (lane == 0) J.state[sd] = st;
 }
 

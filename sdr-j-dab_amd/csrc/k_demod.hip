@@ -1,5 +1,11 @@
-// k_demod.hip -- ofdmDecoder::processToken x 75 per frame (ofdm-decoder.cpp:167-190)
-// + the FreqCorr guard correlation (ofdm-processor.cpp:424-438), for gfx950.
+// k_demod.hip -- the OFDM front end of a frame on one 256-thread workgroup, gfx950:
+//   k_demod_wg<GEN, SYNC>  phaseReference::findIndex (phasereference.cpp:60-88, SYNC),
+//                          get_snr of block 0 (ofdm-decoder.cpp:212-230) and
+//                          ofdmDecoder::processToken x 75 (ofdm-decoder.cpp:167-190)
+//                          + the FreqCorr guard correlation (ofdm-processor.cpp:424-438)
+//   k_prs_wg<GEN>          findIndex alone (frames whose block 0 the host must see first)
+//   k_block0_wg<GEN>       ofdmDecoder::processBlock_0 (ofdm-decoder.cpp:85-162): get_snr
+//                          and the coarse offset, freqSyncMethod 0, 1 or 2
 //
 // One workgroup of 256 threads (4 waves) per (frame, chunk of symbols).  The
 // 2048-point FFT of a symbol is shared by the workgroup, 8 points per thread:
@@ -152,43 +158,185 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
     }
 }
 
-template <bool GEN>
+
+// twiddle tables of fft2048_wg in LDS, laid out per pass so that a wave's reads are
+// conflict-free (the values are the W2048 table's entries: W256^j = W2048^(8 j),
+// W32^j = W2048^(64 j))
+struct TwLds {
+    float2 w1[7 * DT];      // pass 1: LDS instead of 14 VGPRs (room for the guard prefetch)
+    float2 w2[7 * 32];
+    float2 w3[7 * 4];
+};
+__device__ __forceinline__ DemodTw tw_setup(TwLds &L, const OfdmTables &T, int t) {
+#pragma unroll
+    for (int k = 1; k < 8; k++) L.w1[(k - 1) * DT + t] = T.w2048[(t * k) & 2047];
+    if (t < 7 * 32) L.w2[t] = T.w2048[(8 * ((t & 31) * (t / 32 + 1))) & 2047];
+    if (t < 7 * 4) L.w3[t] = T.w2048[(64 * ((t & 3) * (t / 4 + 1))) & 2047];
+    DemodTw tw;
+    const int tq = t & 3;
+    tw.w1 = L.w1;
+    tw.w2 = L.w2;
+    tw.w3 = L.w3;
+    tw.sg2 = (tq & 2) ? -1.0f : 1.0f;
+    tw.sg1 = (tq & 1) ? -1.0f : 1.0f;
+    tw.rot = tq == 3;
+    return tw;
+}
+// FFT bin held in a[k3] by thread t after fft2048_wg
+__device__ __forceinline__ int bin0_of(int t) {
+    const int g = t >> 2, tq = t & 3, k1 = g >> 3, k2 = g & 7;
+    return k1 + 8 * k2 + 512 * (((tq & 1) << 1) | (tq >> 1));
+}
+
+// workgroup reductions (4 waves): sum of floats; max with the lowest index on ties
+struct RedLds {
+    float f[2 * (DT / 64)];
+    int32_t i[DT / 64];
+};
+__device__ __forceinline__ float wg_sum(float v, RedLds &R, int t, int slot) {
+    v = wave_sum(v);
+    if ((t & 63) == 0) R.f[slot * (DT / 64) + (t >> 6)] = v;
+    __syncthreads();
+    float r = R.f[slot * (DT / 64)];
+#pragma unroll
+    for (int w = 1; w < DT / 64; w++) r += R.f[slot * (DT / 64) + w];
+    return r;
+}
+__device__ __forceinline__ void wg_argmax(float &best, int &bidx, RedLds &R, int t) {
+    for (int o = 32; o > 0; o >>= 1) {
+        const float ob = __shfl_xor(best, o);
+        const int oi = __shfl_xor(bidx, o);
+        if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+    }
+    __syncthreads();
+    if ((t & 63) == 0) { R.f[t >> 6] = best; R.i[t >> 6] = bidx; }
+    __syncthreads();
+    best = R.f[0];
+    bidx = R.i[0];
+#pragma unroll
+    for (int w = 1; w < DT / 64; w++)
+        if (R.f[w] > best || (R.f[w] == best && R.i[w] < bidx)) { best = R.f[w]; bidx = R.i[w]; }
+}
+
+// findIndex (phasereference.cpp:60-88) of the T_u window in a[] (n = t + 256 m, mixed):
+// X = FFT(x); r = IFFT(X conj(ref)) = conj(FFT(conj(X conj(ref)))) / 2048; argmax |r|
+// with the first index on ties; -|Max / mean| - 1 when Max < level * mean.
+// Returns startIndex on every thread.
+__device__ __forceinline__ int32_t prs_corr_wg(float2 (&a)[8], float2 *ex, const DemodTw &tw, int t,
+                                               const float2 *__restrict__ ref, int level, RedLds &R,
+                                               float &maxv, float &sumv) {
+    fft2048_wg(a, ex, tw, t);
+    const int b0 = bin0_of(t);
+    __syncthreads();                                     // pass 3 of the FFT read ex
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int b = b0 + 64 * k;
+        const float2 r = cmul_conj_exact(a[k], ref[b]);
+        ex[b] = make_float2(r.x, -r.y);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int m = 0; m < 8; m++) a[m] = ex[t + 256 * m];
+    __syncthreads();
+    fft2048_wg(a, ex, tw, t);
+    constexpr float scale = 1.0f / 2048.0f;            // common_ifft::Scale (fft.cpp:115-121), exact
+    float sum = 0.0f, best = -10000.0f;
+    int bidx = 0x7fffffff;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {                        // increasing time index per thread
+        const float v = hypotf(a[k].x * scale, -a[k].y * scale);
+        sum += v;
+        if (v > best) { best = v; bidx = b0 + 64 * k; }
+    }
+    sum = wg_sum(sum, R, t, 1);
+    wg_argmax(best, bidx, R, t);
+    maxv = best;
+    sumv = sum;
+    if (best < (float)level * sum / 2048.0f) return (int32_t)(-fabsf(best / (sum / 2048.0f)) - 1.0f);
+    return bidx;
+}
+
+// get_snr (ofdm-decoder.cpp:212-230) of the block-0 spectrum in a[] (bins b0 + 64 k):
+// noise = mean |X| over bins 1034..1259 and 788..1013, signal = mean over 1664..2047 and
+// 0..383; get_db(signal) - get_db(noise) with get_db(x) = 20 log10((x + 1) / 256)
+// (dab-constants.h:107-109).  The sums are workgroup trees (the reference adds in bin
+// order): a display value, equal to the sequential one except within float rounding
+// of a dB boundary.
+__device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R) {
+    const int b0 = bin0_of(t);
+    float noise = 0.0f, signal = 0.0f;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int b = b0 + 64 * k;
+        const float v = hypotf(a[k].x, a[k].y);
+        if ((b >= 1034 && b < 1260) || (b >= 788 && b < 1014)) noise += v;
+        if (b >= 1664 || b < 384) signal += v;
+    }
+    noise = wg_sum(noise, R, t, 0);
+    __syncthreads();
+    signal = wg_sum(signal, R, t, 1);
+    noise /= 452;
+    const float db_s = 20 * log10f((signal / 768 + 1) / (float)256);
+    const float db_n = 20 * log10f((noise + 1) / (float)256);
+    return (int16_t)(db_s - db_n);
+}
+
+// The soft bits of symbol l leave through an LDS stage of 1536 {re, im} int16 pairs
+// (one 32-bit write per carrier), read back by carrier quads as 16-byte words and
+// stored as 8-byte re / im groups: output rows stay [3072] = re[1536] | im[1536].
+constexpr int STG = K + DT;                              // + one dump slot per thread
+
+template <bool GEN, bool SYNC>
 __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2 *__restrict__ iq,
                                                     const dabgpu_frame *__restrict__ frames, int nchunks,
                                                     OfdmTables T, int16_t *__restrict__ soft,
                                                     float *__restrict__ softf, float2 *__restrict__ fcpart,
-                                                    const int32_t *__restrict__ si) {
+                                                    DemodAux aux) {
     __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
-    __shared__ int16_t st[2 * K + 2 * DT];
+    __shared__ uint32_t st[STG];
     __shared__ float2 fcw[DT / 64];
-    // twiddles, laid out per pass so that a wave's reads are conflict-free (the values
-    // are the W2048 table's entries: W256^j = W2048^(8 j), W32^j = W2048^(64 j))
-    __shared__ float2 w1s[7 * DT];      // pass 1: LDS instead of 14 VGPRs (room for the guard prefetch)
-    __shared__ float2 w2s[7 * 32];
-    __shared__ float2 w3s[7 * 4];
+    __shared__ TwLds twl;
+    __shared__ RedLds red;
     const int t = threadIdx.x;
-#pragma unroll
-    for (int k = 1; k < 8; k++) w1s[(k - 1) * DT + t] = T.w2048[(t * k) & 2047];
-    if (t < 7 * 32) w2s[t] = T.w2048[(8 * ((t & 31) * (t / 32 + 1))) & 2047];
-    if (t < 7 * 4) w3s[t] = T.w2048[(64 * ((t & 3) * (t / 4 + 1))) & 2047];
+    const DemodTw tw = tw_setup(twl, T, t);
     __syncthreads();
     const int item = blockIdx.x;
     const int fi = item / nchunks, ch = item % nchunks;
     dabgpu_frame fr = frames[fi];
-    // FRAME_SI_ON_DEVICE: the frame starts where k_prs_sync found it (block0 = window +
-    // startIndex, ofdm-processor.cpp:360-368) -- no host round trip between the two;
-    // a frame whose sync failed or whose symbols are not all there yet is skipped
-    // (the host's replay does not commit it)
+    const float2 *s = iq + fr.iq_base;
     bool skip = false;
-    if (si && (fr.flags & FRAME_SI_ON_DEVICE)) {
-        const int32_t s = si[fi];
-        if (s < 0) {
+    if constexpr (SYNC) {
+        // the frame starts where findIndex finds it (block0 = window + startIndex,
+        // ofdm-processor.cpp:344-368): every chunk of the frame correlates the window
+        // itself, chunk 0 reports.  A frame whose sync fails, or whose symbols are not
+        // all there yet, is skipped (the host's replay does not commit it).
+        if (fr.window < 0 || fr.window + TU > fr.n_samples || fr.lp_window < 0 || fr.lp_window >= INPUT_RATE) {
+            if (t == 0) {
+                atomicOr(T.err, KERR_FRAME);
+                if (ch == 0) aux.si[fi] = -1;
+            }
             skip = true;
         } else {
-            fr.block0 = fr.window + s;
-            const int64_t m = ((int64_t)fr.lp_window - ((int64_t)TU + s) * (int64_t)fr.phase_a) % INPUT_RATE;
-            fr.lp_data = (int32_t)(m < 0 ? m + INPUT_RATE : m);
-            skip = fr.block0 + TU + (int64_t)NSYM * TS > fr.n_samples;
+            float2 a[8];
+#pragma unroll
+            for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
+            mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
+            float mx, sm;
+            const int32_t si = prs_corr_wg(a, ex, tw, t, T.ref, aux.level, red, mx, sm);
+            if (ch == 0 && t == 0) {
+                aux.si[fi] = si;
+                if (aux.maxv) aux.maxv[fi] = mx;
+                if (aux.sumv) aux.sumv[fi] = sm;
+            }
+            if (si < 0) {
+                skip = true;
+            } else {
+                fr.block0 = fr.window + si;
+                const int64_t m = ((int64_t)fr.lp_window - ((int64_t)TU + si) * (int64_t)fr.phase_a) % INPUT_RATE;
+                fr.lp_data = (int32_t)(m < 0 ? m + INPUT_RATE : m);
+                skip = fr.block0 + TU + (int64_t)NSYM * TS > fr.n_samples;
+            }
+            __syncthreads();                             // ex reused below
         }
     }
     const int per = (NSYM + nchunks - 1) / nchunks;
@@ -199,30 +347,18 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                     fr.lp_window >= 0 && fr.lp_window < INPUT_RATE && fr.lp_data >= 0 && fr.lp_data < INPUT_RATE;
     if (!ok && !skip && t == 0) atomicOr(T.err, KERR_FRAME);
     if (l0 <= NSYM && ok && !skip) {
-        const float2 *s = iq + fr.iq_base;
         const int64_t dorg = fr.block0 + TU;           // first sample of segment B
-        DemodTw tw;
-        {
-            const int tq = t & 3;
-            tw.w2 = w2s;
-            tw.w3 = w3s;
-            tw.w1 = w1s;
-            tw.sg2 = (tq & 2) ? -1.0f : 1.0f;
-            tw.sg1 = (tq & 1) ? -1.0f : 1.0f;
-            tw.rot = tq == 3;
-        }
         // carriers of this thread's 8 bins (-1: none), two int16 per register
         uint32_t cb[4];
         {
-            const int g = t >> 2, tq = t & 3, k1 = g >> 3, k2 = g & 7;
-            const int kk = ((tq & 1) << 1) | (tq >> 1);
+            const int b0 = bin0_of(t);
 #pragma unroll
             for (int k3 = 0; k3 < 8; k3 += 2)
-                cb[k3 >> 1] = (uint32_t)(uint16_t)T.carrier_of_bin[k1 + 8 * k2 + 64 * k3 + 512 * kk] |
-                              ((uint32_t)(uint16_t)T.carrier_of_bin[k1 + 8 * k2 + 64 * (k3 + 1) + 512 * kk] << 16);
+                cb[k3 >> 1] = (uint32_t)(uint16_t)T.carrier_of_bin[b0 + 64 * k3] |
+                              ((uint32_t)(uint16_t)T.carrier_of_bin[b0 + 64 * (k3 + 1)] << 16);
         }
         float2 a[8], nx[8], P[8], ng6, ng7;
-        // warm-up symbol l0 - 1 (the PRS for the first chunk)
+        // warm-up symbol l0 - 1 (block 0, the PRS, for the first chunk)
         {
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
 #pragma unroll
@@ -238,6 +374,10 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             for (int m = 0; m < 8; m++) nx[m] = s[u + t + 256 * m];
         }
         fft2048_wg(a, ex, tw, t);
+        if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
+            const int16_t v = snr_wg(a, t, red);
+            if (t == 0) aux.snr[fi] = v;
+        }
 #pragma unroll
         for (int k = 0; k < 8; k++) P[k] = a[k];
         for (int l = l0; l < l1; l++) {
@@ -271,20 +411,25 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             for (int k = 0; k < 8; k++) {
                 const float2 r1 = cmul_conj_exact(a[k], P[k]);
                 P[k] = a[k];
-                // q = -re / (|re| + |im|): one reciprocal for both (<= 1 ulp; the FFT
-                // before it already differs from FFTW3f's by more)
-                const float inv = __builtin_amdgcn_rcpf(fabsf(r1.x) + fabsf(r1.y));
-                const float qr = -r1.x * inv, qi = -r1.y * inv;
+                // q = -re / ab1, ab1 = |re| + |im| (jan_abs): two IEEE divisions, as the
+                // reference (ofdm-decoder.cpp:185-189; HIP divides correctly rounded)
+                const float ab1 = fabsf(r1.x) + fabsf(r1.y);
+                const float qr = -r1.x / ab1, qi = -r1.y / ab1;
                 const int c = (int)(int16_t)((k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu));
-                st[c >= 0 ? c : 2 * K + t] = (int16_t)trunc127d(qr);
-                st[c >= 0 ? K + c : 2 * K + DT + t] = (int16_t)trunc127d(qi);
+                st[c >= 0 ? c : K + t] = (uint32_t)(uint16_t)(int16_t)trunc127d(qr) |
+                                         ((uint32_t)(uint16_t)(int16_t)trunc127d(qi) << 16);
                 if (sf && c >= 0) { sf[c] = qr; sf[K + c] = qi; }
             }
             __syncthreads();
-            int2 *dst = (int2 *)(soft + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS);
-            const int2 *src = (const int2 *)st;
-#pragma unroll
-            for (int i = 0; i < 3; i++) dst[t + DT * i] = src[t + DT * i];
+            int16_t *row = soft + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS;
+            // carriers 4q..4q+3, q < 384: re to row[4q..], im to row[K + 4q..]
+            for (int q = t; q < K / 4; q += DT) {
+                const uint4 w = ((const uint4 *)st)[q];
+                const uint2 re = make_uint2((w.x & 0xFFFFu) | (w.y << 16), (w.z & 0xFFFFu) | (w.w << 16));
+                const uint2 im = make_uint2((w.x >> 16) | (w.y & 0xFFFF0000u), (w.z >> 16) | (w.w & 0xFFFF0000u));
+                ((uint2 *)row)[q] = re;
+                ((uint2 *)(row + K))[q] = im;
+            }
             __syncthreads();
         }
     }
@@ -299,17 +444,182 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     }
 }
 
+// findIndex alone, one workgroup per frame (the host needs startIndex before block 0
+// while the coarse AFC is pending)
+template <bool GEN>
+__global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
+                                               OfdmTables T, DemodAux aux) {
+    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ TwLds twl;
+    __shared__ RedLds red;
+    const int t = threadIdx.x, f = blockIdx.x;
+    const DemodTw tw = tw_setup(twl, T, t);
+    __syncthreads();
+    const dabgpu_frame fr = frames[f];
+    if (fr.window < 0 || fr.window + TU > fr.n_samples || fr.lp_window < 0 || fr.lp_window >= INPUT_RATE) {
+        if (t == 0) {
+            atomicOr(T.err, KERR_FRAME);
+            aux.si[f] = -1;
+        }
+        return;
+    }
+    const float2 *s = iq + fr.iq_base;
+    float2 a[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
+    mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
+    float mx, sm;
+    const int32_t si = prs_corr_wg(a, ex, tw, t, T.ref, aux.level, red, mx, sm);
+    if (t == 0) {
+        aux.si[f] = si;
+        if (aux.maxv) aux.maxv[f] = mx;
+        if (aux.sumv) aux.sumv[f] = sm;
+    }
+}
+
+// processBlock_0 (ofdm-decoder.cpp:85-162), one workgroup per frame: FFT of block 0
+// (segment A of the NCO), get_snr, and when frames[f].flags & 1 the coarse offset of
+// freqSyncMethod `method` in carriers (100 - 2048 when method 2 finds nothing, 100
+// means "no estimate" for method 1 -- the reference's values).
+template <bool GEN>
+__global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
+                                                  OfdmTables T, int method, int16_t *__restrict__ correction,
+                                                  int16_t *__restrict__ snr) {
+#pragma clang fp contract(off)
+    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ TwLds twl;
+    __shared__ RedLds red;
+    __shared__ float val[2048];                          // |X| (method 0) or per-candidate sums
+    __shared__ float cv[96];                             // method 1: correlationVector
+    const int t = threadIdx.x, f = blockIdx.x;
+    const DemodTw tw = tw_setup(twl, T, t);
+    __syncthreads();
+    const dabgpu_frame fr = frames[f];
+    if (fr.window < 0 || fr.block0 < fr.window || fr.block0 + TU > fr.n_samples || fr.lp_window < 0 ||
+        fr.lp_window >= INPUT_RATE) {
+        if (t == 0) {
+            atomicOr(T.err, KERR_FRAME);
+            correction[f] = 0;
+            if (snr) snr[f] = 0;
+        }
+        return;
+    }
+    const float2 *s = iq + fr.iq_base;
+    float2 a[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) a[m] = s[fr.block0 + t + 256 * m];
+    mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, fr.block0 + t, fr.window);
+    fft2048_wg(a, ex, tw, t);
+    {
+        const int16_t v = snr_wg(a, t, red);
+        if (t == 0 && snr) snr[f] = v;
+    }
+    if (!(fr.flags & 1)) {                               // f2Correction off: no estimate
+        if (t == 0) correction[f] = 0;
+        return;
+    }
+    __syncthreads();
+    const int b0 = bin0_of(t);
+#pragma unroll
+    for (int k = 0; k < 8; k++) ex[b0 + 64 * k] = a[k];  // natural bin order
+    if (method == 0) {
+#pragma unroll
+        for (int k = 0; k < 8; k++) val[b0 + 64 * k] = hypotf(a[k].x, a[k].y);
+    }
+    __syncthreads();
+    auto argpair = [&](int i, int j) -> float {          // arg (X[i] conj(X[j]))
+        const float2 p = cmul_conj_exact(ex[i & 2047], ex[j & 2047]);
+        return atan2f(p.y, p.x);
+    };
+    if (method == 1) {                                   // ofdm-decoder.cpp:106-127
+        if (t < 72 + 18) cv[t] = argpair(2048 - 36 + t, 2048 - 36 + t + 1);
+        __syncthreads();
+        if (t < 72) {
+            float sum = 0.0f;
+            for (int j = 1; j < 18; j++) sum += fabsf(T.refarg[j] * cv[t + j]);
+            val[t] = sum;
+        }
+        __syncthreads();
+        if (t == 0) {
+            float MMax = 0.0f;
+            int index = 100;
+            for (int i = 0; i < 72; i++)
+                if (val[i] > MMax) { MMax = val[i]; index = i; }
+            correction[f] = (int16_t)(2048 - 36 + index - 2048);
+        }
+    } else if (method == 2) {                            // ofdm-decoder.cpp:128-161
+        if (t < 72) {
+            const int i = 2048 - 36 + t;
+            const double pi = M_PI;
+            const float a1 = (float)fabs(fabs((double)argpair(i + 1, i + 2) / pi) - 1);
+            const float a2 = (float)fabs(fabs((double)argpair(i + 2, i + 3) / pi) - 1);
+            const float a3 = fabsf(argpair(i + 3, i + 4));
+            const float a4 = fabsf(argpair(i + 4, i + 5));
+            const float a5 = fabsf(argpair(i + 5, i + 6));
+            const float c1 = (float)fabs(fabs((double)argpair(i + 17, i + 19) / pi) - 1);
+            const float c2 = fabsf(argpair(i + 19, i + 20));
+            const float c3 = fabsf(argpair(i + 20, i + 21));
+            const float c4 = fabsf(argpair(i + 21, i + 22));
+            val[t] = a1 + a2 + a3 + a4 + a5 + c1 + c2 + c3 + c4;
+        }
+        __syncthreads();
+        if (t == 0) {
+            float Mmin = 1000.0f;
+            int index = 100;
+            for (int k = 0; k < 72; k++)
+                if (val[k] < Mmin) { Mmin = val[k]; index = 2048 - 36 + k; }
+            correction[f] = (int16_t)(index - 2048);
+        }
+    } else {                                             // getMiddle (ofdm-decoder.cpp:233-258), sequential
+        if (t == 0) {
+            float sum = 0.0f, oldMax = 0.0f;
+            int maxIndex = 0;
+            for (int i = 40; i < 1536 + 40; i++) sum += val[(1024 + i) & 2047];
+            for (int i = 40; i < 2048 - (1536 - 40); i++) {
+                sum -= val[(1024 + i) & 2047];
+                sum += val[(1024 + i + 1536) & 2047];
+                if (sum > oldMax) { sum = oldMax; maxIndex = i; }
+            }
+            correction[f] = (int16_t)(maxIndex - (2048 - 1536) / 2);
+        }
+    }
+}
+
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
-                        const int32_t *si) {
+                        const DemodAux &aux) {
     if (n <= 0) return hipSuccess;
     const dim3 grid(n * nchunks), block(DT);
-    if (general)
-        hipLaunchKernelGGL(k_demod_wg<true>, grid, block, 0, st, (const float2 *)iq, fr, nchunks, T, soft, softf,
-                           (float2 *)fcpart, si);
-    else
-        hipLaunchKernelGGL(k_demod_wg<false>, grid, block, 0, st, (const float2 *)iq, fr, nchunks, T, soft, softf,
-                           (float2 *)fcpart, si);
+    const float2 *x = (const float2 *)iq;
+    float2 *fp = (float2 *)fcpart;
+    if (aux.si) {
+        if (general) hipLaunchKernelGGL((k_demod_wg<true, true>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
+        else hipLaunchKernelGGL((k_demod_wg<false, true>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
+    } else {
+        if (general) hipLaunchKernelGGL((k_demod_wg<true, false>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
+        else hipLaunchKernelGGL((k_demod_wg<false, false>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+                           int level, int32_t *si, float *mx, float *sm, bool general) {
+    if (n <= 0) return hipSuccess;
+    DemodAux aux{};
+    aux.si = si;
+    aux.maxv = mx;
+    aux.sumv = sm;
+    aux.level = level;
+    if (general) hipLaunchKernelGGL(k_prs_wg<true>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, aux);
+    else hipLaunchKernelGGL(k_prs_wg<false>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, aux);
+    return hipGetLastError();
+}
+
+hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+                         int method, int16_t *corr, int16_t *snr, bool general) {
+    if (n <= 0) return hipSuccess;
+    if (general) hipLaunchKernelGGL(k_block0_wg<true>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, method, corr, snr);
+    else hipLaunchKernelGGL(k_block0_wg<false>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, method, corr, snr);
     return hipGetLastError();
 }
 

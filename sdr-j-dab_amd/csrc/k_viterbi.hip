@@ -85,7 +85,9 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
         c.base = J.src + (int64_t)logical * J.src_stride;
         c.prof = J.cw_prof ? J.cw_prof[logical] : 0;
     } else if constexpr (KIND == SRC_FIC) {
-        c.base = J.src + (int64_t)J.slots[logical >> 2] * FRAME_SOFT + (logical & 3) * 2304;
+        const int32_t slot = J.slots[logical >> 2];    // < 0: frame not committed
+        c.valid = c.valid && slot >= 0;
+        c.base = J.src + (int64_t)(slot < 0 ? 0 : slot) * FRAME_SOFT + (logical & 3) * 2304;
     } else {
         const int cl = logical % J.ncif;
         const int rest = logical / J.ncif;
@@ -93,8 +95,9 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
         const int stream = rest / J.nsub;
         c.row = (stream * J.ncif + cl) * J.nsub + sub;
         c.prof = sub;
-        const int64_t cif = J.cif0 + cl;
-        c.valid = c.valid && cif >= 16;                // dab-concurrent.cpp:172-175 warm-up
+        const int64_t cif = J.cif0s[stream] + cl;
+        // CIFs the stream delivered in this batch; dab-concurrent.cpp:172-175 warm-up
+        c.valid = c.valid && cl < J.ncifs[stream] && cif >= 16;
         c.base = J.src + (int64_t)stream * J.ring * FRAME_SOFT;
         if (lane < 16) {
             // element idx of CIF n comes from CIF n - d[idx & 15] (dab-concurrent.cpp:42-43,162-169)
@@ -270,10 +273,12 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
     typedef short i16x2 __attribute__((ext_vector_type(2)));
     uint32_t y[4];
 #pragma unroll
-    for (int e = 0; e < 4; e++) {                 // clamp(s + 127, 0, 255) per half
-        const i16x2 v = __builtin_elementwise_min(__builtin_elementwise_max(__builtin_bit_cast(i16x2, s[e]),
-                                                                            (i16x2){-127, -127}), (i16x2){128, 128});
-        y[e] = as_u32(__builtin_bit_cast(u16x2, v) + (u16x2){127, 127});
+    for (int e = 0; e < 4; e++) {
+        // int16_t temp = input[i] + 127, clamped to 0..255 (viterbi.cpp:230-233): the sum
+        // wraps in 16 bits like the reference's int16_t, so inputs above 32640 become 0
+        const i16x2 t = __builtin_bit_cast(i16x2, as_u32(s[e] + (u16x2){127, 127}));
+        const i16x2 v = __builtin_elementwise_min(__builtin_elementwise_max(t, (i16x2){0, 0}), (i16x2){255, 255});
+        y[e] = __builtin_bit_cast(uint32_t, v);
     }
     const uint32_t a0 = y[0] + y[3], a1 = 0x01FE01FEu - a0;
     const uint32_t b0 = y[1] + y[2], b1 = 0x00FF00FFu - y[1] + y[2], b2 = 0x00FF00FFu + y[1] - y[2],
@@ -558,10 +563,13 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
         if constexpr (KIND == SRC_MSC) {
             const int sub = cw % J.nsub;
             const int cl = (cw / J.nsub) % J.ncif;
+            const int stream = cw / J.nsub / J.ncif;
             prof = sub;
-            act = J.cif0 + cl >= 16;
+            act = cl < J.ncifs[stream] && J.cif0s[stream] + cl >= 16;
         } else if constexpr (KIND == SRC_FRAG) {
             prof = J.cw_prof ? J.cw_prof[cw] : 0;
+        } else if constexpr (KIND == SRC_FIC) {
+            act = J.slots[cw >> 2] >= 0;
         }
         if (J.valid && !J.valid[cw]) act = false;
         if (act) N = J.prof[prof].nbits;
@@ -743,9 +751,15 @@ __global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) 
 
 // FIB CRC check (dab-constants.h:310-340): invert the 16 CRC bits in place, run
 // CRC-CCITT from all-ones over 256 bits, pass iff the register ends at zero.
-__global__ void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok, int n_fib) {
+// slots (optional): ring slot per frame (12 FIBs), < 0 = frame not committed: no check, ok = 0
+__global__ void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok, int n_fib,
+                           const int32_t *__restrict__ slots) {
     const int f = blockIdx.x * blockDim.x + threadIdx.x;
     if (f >= n_fib) return;
+    if (slots && slots[f / 12] < 0) {
+        ok[f] = 0;
+        return;
+    }
     uint8_t *b = bits + (int64_t)f * 256;
     for (int i = 240; i < 256; i++) b[i] ^= 1;
     uint32_t r = 0xFFFF;
@@ -804,9 +818,9 @@ hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJo
     return hipGetLastError();
 }
 
-hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib) {
+hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib, const int32_t *slots) {
     if (n_fib <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fic_post, dim3((n_fib + 63) / 64), dim3(64), 0, st, bits, ok, n_fib);
+    hipLaunchKernelGGL(k_fic_post, dim3((n_fib + 63) / 64), dim3(64), 0, st, bits, ok, n_fib, slots);
     return hipGetLastError();
 }
 

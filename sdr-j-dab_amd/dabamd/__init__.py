@@ -60,7 +60,18 @@ class StreamState(C.Structure):
     _fields_ = [("next_pos", C.c_int64), ("local_phase", C.c_int32), ("coarse", C.c_int32),
                 ("fine", C.c_int16), ("f2correction", C.c_int16), ("prev1", C.c_int16), ("prev2", C.c_int16),
                 ("synced", C.c_int32), ("cif_count", C.c_int64), ("last_start_index", C.c_int32),
-                ("resyncs", C.c_int32)]
+                ("resyncs", C.c_int32), ("acquisitions", C.c_int32), ("attempts", C.c_int32),
+                ("no_signal", C.c_int32), ("frames_run", C.c_int32), ("reserved", C.c_int32)]
+
+
+class FrameInfo(C.Structure):
+    """dabgpu_frame_info: per-frame observables of the last run (ofdm-processor.cpp:344-446,
+    ofdm-decoder.cpp:93-97)"""
+    _fields_ = [("window", C.c_int64), ("start_index", C.c_int32), ("coarse", C.c_int32), ("fine", C.c_int16),
+                ("correction", C.c_int16), ("snr", C.c_int16), ("committed", C.c_int16)]
+
+
+CTL_RESET, CTL_COARSE_ON, CTL_COARSE_OFF, CTL_SCAN_ON, CTL_SCAN_OFF, CTL_RESYNC = 1, 2, 3, 4, 5, 6
 
 
 _lib: Optional[C.CDLL] = None
@@ -76,6 +87,8 @@ def lib() -> C.CDLL:
         vp, i32, i64, sz = C.c_void_p, C.c_int, C.c_int64, C.c_size_t
         sig = {
             "dabgpu_abi_version": ([], i32), "dabgpu_last_error": ([], C.c_char_p),
+            "dabgpu_host_table": ([i32, vp, sz], i32),
+            "dabgpu_subch_profile": ([vp, vp, vp, vp, vp, vp], i32),
             "dabgpu_device_count": ([], i32), "dabgpu_ctx_create": ([i32, C.POINTER(vp)], i32),
             "dabgpu_ctx_destroy": ([vp], i32), "dabgpu_sync": ([vp], i32),
             "dabgpu_alloc": ([vp, sz, C.POINTER(vp)], i32), "dabgpu_free": ([vp, vp], i32),
@@ -86,7 +99,7 @@ def lib() -> C.CDLL:
             "dabgpu_kernel_errors": ([vp], i32),
             "dabgpu_event_elapsed": ([vp, i32, i32, C.POINTER(C.c_float)], i32),
             "dabgpu_prs_sync": ([vp, vp, vp, i32, C.c_int16, vp, vp, vp], i32),
-            "dabgpu_block0": ([vp, vp, vp, i32, vp], i32),
+            "dabgpu_block0": ([vp, vp, vp, i32, i32, vp, vp], i32),
             "dabgpu_ofdm_demod": ([vp, vp, vp, i32, vp, vp, vp], i32),
             "dabgpu_viterbi": ([vp, vp, i32, i32, vp], i32),
             "dabgpu_fic_decode": ([vp, vp, i32, vp, vp], i32),
@@ -99,6 +112,8 @@ def lib() -> C.CDLL:
             "dabgpu_pipe_acquire": ([vp, vp, i64, vp, vp], i32),
             "dabgpu_pipe_run": ([vp, vp, i64, vp, vp, vp, vp, C.c_int32, vp], i32),
             "dabgpu_pipe_state": ([vp, i32, vp], i32),
+            "dabgpu_pipe_frame_info": ([vp, vp], i32),
+            "dabgpu_pipe_control": ([vp, i32, i32], i32),
             "dabgpu_pipe_softbits": ([vp, C.POINTER(vp), C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frame_slot": ([vp, i32, C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frames": ([vp, vp, vp], i32),
@@ -122,6 +137,27 @@ def _p(a: np.ndarray) -> C.c_void_p:
 
 
 IQ_U8, IQ_S16 = 1, 2   # dabgpu_iq_convert formats
+TABLE_PRS, TABLE_MAPPER, TABLE_REFARG = 1, 2, 3
+
+
+def host_table(which: int) -> np.ndarray:
+    """the product's host-built tables (dabgpu_host_table; no device needed)"""
+    shape, dt = {TABLE_PRS: ((2048, 2), np.float32), TABLE_MAPPER: (1536, np.int16),
+                 TABLE_REFARG: (18, np.float32)}[which]
+    out = np.zeros(shape, dt)
+    _chk(lib().dabgpu_host_table(which, _p(out), out.nbytes), "dabgpu_host_table")
+    return out
+
+
+def subch_profile(sub: "Subch"):
+    """(nbits, fragment size, [(L_i, PI_i)...], fallback) of the decoder's depuncturing
+    profile for a subchannel (dabgpu_subch_profile)"""
+    nb, fr, ns = C.c_int32(), C.c_int32(), C.c_int32()
+    L, PI = np.zeros(4, np.int32), np.zeros(4, np.int32)
+    rc = lib().dabgpu_subch_profile(C.byref(sub), C.byref(nb), C.byref(fr), C.byref(ns), _p(L), _p(PI))
+    if rc < 0:
+        _chk(rc, "dabgpu_subch_profile")
+    return nb.value, fr.value, [(int(L[k]), int(PI[k])) for k in range(ns.value)], rc == 1
 
 
 def read_raw(path: str) -> np.ndarray:
@@ -349,19 +385,21 @@ class Context:
             for b in (dfr, dsi, dmx, dsm):
                 b.free()
 
-    def block0(self, iq: DevBuf, frames: Sequence[Frame]) -> np.ndarray:
-        """ofdmDecoder::processBlock_0 coarse offset (ofdm-decoder.cpp:85-127)."""
+    def block0(self, iq: DevBuf, frames: Sequence[Frame], method: int = 1, with_snr: bool = False):
+        """ofdmDecoder::processBlock_0 (ofdm-decoder.cpp:85-162): coarse offset of
+        freqSyncMethod `method` (frames with flags & 1), and get_snr when with_snr."""
         n = len(frames)
         fa = (Frame * n)(*frames)
         dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
-        dc = self.buf(2 * n)
+        dc, ds = self.buf(2 * n), self.buf(2 * n)
         try:
-            _chk(lib().dabgpu_block0(self.h, iq.ptr, dfr.ptr, n, dc.ptr), "block0")
+            _chk(lib().dabgpu_block0(self.h, iq.ptr, dfr.ptr, n, method, dc.ptr, ds.ptr), "block0")
             r = dc.download(np.int16, n)
+            snr = ds.download(np.int16, n)
             self.check()
-            return r
+            return (r, snr) if with_snr else r
         finally:
-            dfr.free(); dc.free()
+            dfr.free(); dc.free(); ds.free()
 
     def demod(self, iq: DevBuf, frames: Sequence[Frame], with_float: bool = False):
         """ofdmDecoder::processToken for symbols 1..75 (ofdm-decoder.cpp:167-190).
@@ -421,14 +459,17 @@ class Pipeline:
         na = np.asarray(n_avail, dtype=np.int64)
         _chk(lib().dabgpu_pipe_acquire(self.h, iq.ptr, stride, _p(st), _p(na)), "dabgpu_pipe_acquire")
 
-    def run(self, iq: DevBuf, stride: int, n_avail: Sequence[int], download: bool = True):
+    def run(self, iq: DevBuf, stride: int, n_avail: Sequence[int], download: bool = True, partial: bool = False):
+        """one dabgpu_pipe_run; partial=True accepts a run in which a stream ran out of
+        samples (DABGPU_E_STATE: its decoded frames are still delivered)"""
         na = np.asarray(n_avail, dtype=np.int64)
         valid = np.zeros((self.S, 4 * self.F), dtype=np.uint8)
         self.fic_d, self.crc_d, self.msc_d = self._outs[self._run & 1]
         self._run += 1
-        _chk(lib().dabgpu_pipe_run(self.h, iq.ptr, stride, _p(na), self.fic_d.ptr, self.crc_d.ptr,
-                                   self.msc_d.ptr if self.subch else None, self.msc_stride, _p(valid)),
-             "dabgpu_pipe_run")
+        rc = lib().dabgpu_pipe_run(self.h, iq.ptr, stride, _p(na), self.fic_d.ptr, self.crc_d.ptr,
+                                   self.msc_d.ptr if self.subch else None, self.msc_stride, _p(valid))
+        if not (partial and rc == -6):
+            _chk(rc, "dabgpu_pipe_run")
         if not download:
             return valid
         self.sync()
@@ -475,6 +516,17 @@ class Pipeline:
         o = StreamState()
         _chk(lib().dabgpu_pipe_state(self.h, s, C.byref(o)), "dabgpu_pipe_state")
         return o
+
+    def frame_info(self):
+        """[S][F] FrameInfo records of the last run"""
+        n = self.S * self.F
+        fi = (FrameInfo * n)()
+        _chk(lib().dabgpu_pipe_frame_info(self.h, C.cast(fi, C.c_void_p)), "dabgpu_pipe_frame_info")
+        return [list(fi)[s * self.F:(s + 1) * self.F] for s in range(self.S)]
+
+    def control(self, op: int, stream: int = -1) -> None:
+        """ofdmProcessor's reset / coarseCorrectorOn/Off / set_scanMode (dabgpu_pipe_control)"""
+        _chk(lib().dabgpu_pipe_control(self.h, stream, op), "dabgpu_pipe_control")
 
     def frames(self):
         n = self.S * self.F

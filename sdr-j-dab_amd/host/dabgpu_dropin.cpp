@@ -222,13 +222,20 @@ void ensembleDecoder::load(const std::vector<const DSPCOMPLEX *> &samples, const
                               sizeof(float) * 2 * n[s]),
             "dabgpu_memcpy_h2d");
     navail_ = n;
-    frames_done_ = 0;
+    frames_done_.assign(cfg_.n_streams, 0);
 }
 
 void ensembleDecoder::acquire() {
+    // unsynchronised streams search from where they are (sample 0 for a new decoder,
+    // the position after a sync loss otherwise: notSynced continues, ofdm-processor.cpp:274)
     std::vector<int64_t> start(cfg_.n_streams, 0);
-    chk(dabgpu_pipe_acquire(pipe_, (const float *)iq_.get(), stride_, start.data(), navail_.data()),
-        "dabgpu_pipe_acquire");
+    for (int s = 0; s < cfg_.n_streams; s++) {
+        dabgpu_stream_state st;
+        chk(dabgpu_pipe_state(pipe_, s, &st), "dabgpu_pipe_state");
+        start[s] = st.next_pos;
+    }
+    const int rc = dabgpu_pipe_acquire(pipe_, (const float *)iq_.get(), stride_, start.data(), navail_.data());
+    if (rc != DABGPU_OK && rc != DABGPU_E_STATE) chk(rc, "dabgpu_pipe_acquire");
 }
 
 bool ensembleDecoder::step() {
@@ -240,34 +247,34 @@ bool ensembleDecoder::step() {
     if (rc != DABGPU_OK && rc != DABGPU_E_STATE) chk(rc, "dabgpu_pipe_run");
     const bool ok = rc == DABGPU_OK;
     chk(dabgpu_pipe_sync(pipe_), "dabgpu_pipe_sync");
-    // frames committed per stream: FIC is delivered for those, MSC only on success
-    std::vector<dabgpu_frame> fr((size_t)S * F);
-    std::vector<int32_t> si((size_t)S * F);
-    chk(dabgpu_pipe_frames(pipe_, fr.data(), si.data()), "dabgpu_pipe_frames");
+    // frames committed per stream (a stream that lost sync re-acquired inside the run;
+    // one that ran out of samples committed fewer): FIC and MSC for those
+    std::vector<dabgpu_frame_info> fr((size_t)S * F);
+    chk(dabgpu_pipe_frame_info(pipe_, fr.data()), "dabgpu_pipe_frame_info");
     std::vector<uint8_t> fic((size_t)S * F * 4 * 768), crc((size_t)S * F * 12);
     fic_.download(fic.data(), fic.size());
     crc_.download(crc.data(), crc.size());
     for (int s = 0; s < S && fib_cb_; s++)
         for (int f = 0; f < F; f++) {
-            if (fr[(size_t)s * F + f].window == 0) continue;   // not committed in this run
+            if (!fr[(size_t)s * F + f].committed) continue;
             for (int b = 0; b < 4; b++)
                 for (int k = 0; k < 3; k++) {
                     const size_t o = (((size_t)s * F + f) * 4 + b) * 768 + 256 * k;
-                    fib_cb_(s, frames_done_ + f, b, fic.data() + o, crc[((size_t)s * F + f) * 12 + 3 * b + k] != 0);
+                    fib_cb_(s, frames_done_[s] + f, b, fic.data() + o, crc[((size_t)s * F + f) * 12 + 3 * b + k] != 0);
                 }
         }
-    if (ok && NS && msc_cb_) {
+    if (NS && msc_cb_) {
         std::vector<uint8_t> msc((size_t)S * 4 * F * NS * msc_stride_);
         msc_.download(msc.data(), msc.size());
         for (int s = 0; s < S; s++)
             for (int c = 0; c < 4 * F; c++) {
                 if (!valid[(size_t)s * 4 * F + c]) continue;
                 for (int k = 0; k < NS; k++)
-                    msc_cb_(s, 4 * frames_done_ + c, k, msc.data() + (((size_t)s * 4 * F + c) * NS + k) * msc_stride_,
+                    msc_cb_(s, 4 * frames_done_[s] + c, k, msc.data() + (((size_t)s * 4 * F + c) * NS + k) * msc_stride_,
                          24 * cfg_.subch[k].bitRate);
             }
     }
-    if (ok && ndp_) {
+    if (NS && ndp_) {
         chk(dabgpu_pipe_dabplus(pipe_, (uint8_t *)sf_.get(), sf_stride_, (dabgpu_superframe *)sfi_.get()),
             "dabgpu_pipe_dabplus");
         chk(dabgpu_pipe_sync(pipe_), "dabgpu_pipe_sync");
@@ -282,12 +289,16 @@ bool ensembleDecoder::step() {
                 const int c = (int)((r / ndp_) % (4 * F));
                 const int s = (int)(r / ndp_ / (4 * F));
                 const int k = dp_index_[d];
-                sf_cb_(s, 4 * frames_done_ + c, k, info[r], bytes.data() + r * sf_stride_,
+                sf_cb_(s, 4 * frames_done_[s] + c, k, info[r], bytes.data() + r * sf_stride_,
                     info[r].status == 3 ? 110 * (cfg_.subch[k].bitRate / 8) : 0);
             }
         }
     }
-    if (ok) frames_done_ += F;
+    for (int s = 0; s < S; s++) {
+        dabgpu_stream_state st;
+        chk(dabgpu_pipe_state(pipe_, s, &st), "dabgpu_pipe_state");
+        frames_done_[s] += st.frames_run;
+    }
     return ok;
 }
 

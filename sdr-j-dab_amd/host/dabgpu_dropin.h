@@ -149,10 +149,12 @@ public:
     void on_superframe(sf_cb f) { sf_cb_ = std::move(f); }
     // samples[s] -> n[s] cf32 samples of stream s (copied to HBM)
     void load(const std::vector<const DSPCOMPLEX *> &samples, const std::vector<int64_t> &n);
-    // null search from sample 0 of every stream (ofdm-processor.cpp:274-338)
+    // null search (ofdm-processor.cpp:274-338) for every unsynchronised stream from its
+    // current position (optional: step() acquires such streams itself)
     void acquire();
-    // decode the next n_frames frames of every stream; false when a stream lost
-    // sync or ran out of samples (the frames before that were delivered)
+    // decode the next n_frames frames of every stream (a stream that loses sync searches
+    // the next null symbol and continues, as ofdmProcessor::run); false when a stream
+    // ran out of samples (the frames it decoded were delivered)
     bool step();
     dabgpu_stream_state state(int stream) const;
 private:
@@ -163,7 +165,7 @@ private:
     std::vector<int64_t> navail_;
     int msc_stride_ = 0, sf_stride_ = 0, ndp_ = 0;
     std::vector<int> dp_index_;
-    int64_t frames_done_ = 0;
+    std::vector<int64_t> frames_done_;     // frames delivered per stream
     fib_cb fib_cb_;
     msc_cb msc_cb_;
     sf_cb sf_cb_;

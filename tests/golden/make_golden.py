@@ -19,6 +19,55 @@ from dabamd.synth import conv_encode  # noqa: E402
 P = oracle_py.P
 
 
+UEP_ROWS = [(32, 5), (32, 4), (32, 3), (32, 2), (32, 1), (48, 5), (48, 4), (48, 3), (48, 2), (48, 1),
+            (64, 5), (64, 4), (64, 3), (64, 2), (64, 1), (80, 5), (80, 4), (80, 3), (80, 2), (80, 1),
+            (96, 5), (96, 4), (96, 3), (96, 2), (96, 1), (112, 5), (112, 4), (112, 3), (112, 2),
+            (128, 5), (128, 4), (128, 3), (128, 2), (128, 1), (160, 5), (160, 4), (160, 3), (160, 2), (160, 1),
+            (192, 5), (192, 4), (192, 3), (192, 2), (192, 1), (224, 5), (224, 4), (224, 3), (224, 2), (224, 1),
+            (256, 5), (256, 4), (256, 3), (256, 2), (256, 1), (320, 5), (320, 4), (320, 2),
+            (384, 5), (384, 3), (384, 1)]
+
+
+def profile_cases():
+    """(uepFlag, bitRate, protLevel): uepFlag 0 = UEP (deconvolve.cpp:130)"""
+    cases = [(0, br, pl) for br, pl in UEP_ROWS]
+    cases += [(0, 999, 3), (0, 128, 7), (0, 112, 1)]          # not in the table: row-1 fallback
+    for lvl in (1, 2, 3, 4):                                   # EEP-A: bitRate multiple of 8
+        for br in (8, 16, 24, 64, 136, 384):
+            cases.append((1, br, 0o100 | lvl))
+    for lvl in (1, 2, 3, 4):                                   # EEP-B: bitRate multiple of 32
+        for br in (32, 64, 160, 384):
+            cases.append((1, br, 0o200 | lvl))
+    return cases
+
+
+def profiles_kat(r, rng):
+    cases = profile_cases()
+    assert len(UEP_ROWS) == 60
+    used, frags, outs = [], [], []
+    for uf, br, pl in cases:
+        vb = np.zeros(4 * 24 * br + 24, np.int16)
+        big = rng.integers(-127, 128, 60000).astype(np.int16)
+        n = oracle_py.oracle().orc_msc_depuncture(1 if uf == 0 else 0, br, pl, P(big), P(vb))
+        assert n > 0, (uf, br, pl)
+        frag = np.ascontiguousarray(big[:n])
+        o = np.zeros(24 * br, np.uint8)
+        fn = r.ref_uep_deconvolve if uf == 0 else r.ref_eep_deconvolve
+        fn(br, pl, P(frag), n, P(o))
+        used.append(n)
+        frags.append(frag.astype(np.int8))
+        outs.append(np.packbits(o))
+    m = max(used)
+    fr = np.zeros((len(cases), m), np.int8)
+    for i, f in enumerate(frags):
+        fr[i, :len(f)] = f
+    ob = np.zeros((len(cases), max(len(o) for o in outs)), np.uint8)
+    for i, o in enumerate(outs):
+        ob[i, :len(o)] = o
+    np.savez_compressed(os.path.join(HERE, "profiles_kat.npz"), cases=np.array(cases, np.int32),
+                        used=np.array(used, np.int32), frags=fr, out=ob)
+
+
 def main():
     r = oracle_py.ref()
     if r is None:
@@ -32,6 +81,15 @@ def main():
     ks = np.array(list(range(-768, 0)) + list(range(1, 769)), np.int32)
     out["phi_k"] = ks
     out["phi"] = np.array([r.ref_get_phi(int(k)) for k in ks], np.float32)
+    # refTable[k] = (cos(Phi_k), sin(Phi_k)) in float (phasereference.cpp:40-47): the
+    # reference's std::cos/sin(float) are glibc's cosf/sinf, called here through libm
+    libm = C.CDLL("libm.so.6")
+    libm.cosf.restype = libm.sinf.restype = C.c_float
+    libm.cosf.argtypes = libm.sinf.argtypes = [C.c_float]
+    ref = np.zeros((2048, 2), np.float32)
+    for k, ph in zip(ks, out["phi"]):
+        ref[int(k) % 2048] = (libm.cosf(float(ph)), libm.sinf(float(ph)))
+    out["ref_table"] = ref
     pc = np.zeros((24, 32), np.int8)
     for i in range(24):
         row = np.zeros(32, np.int8)
@@ -94,6 +152,26 @@ def main():
     fire = rng.integers(0, 256, (64, 11)).astype(np.uint8)
     fok = np.array([r.ref_firecode_check(P(fire[i])) for i in range(64)], np.uint8)
     np.savez_compressed(os.path.join(HERE, "crc_kat.npz"), fibs=fibs, crc=crc, mutated=mut, fire=fire, fire_ok=fok)
+    # every protection profile (deconvolve.cpp:39-114 UEP rows, :148-151 the unknown-
+    # profile fallback, :244-314 EEP-A 1-4 incl. the 8 kbit/s case and EEP-B 1-4):
+    # fragments as int8 (soft bits in [-127, 127]), exactly as long as the profile
+    # consumes (the oracle's depuncturing counts them), outputs bit-packed
+    profiles_kat(r, np.random.default_rng(20261016))
+    # int16 extremes (viterbi.cpp:230-233: temp = input + 127 is an int16_t, so inputs
+    # above 32640 wrap to negative and clamp to 0)
+    ext_rng = np.random.default_rng(7)
+    vals = np.array([32767, 32700, 32641, 32640, 32639, -32768, -32767, 300, -300, 128, -128, 127, -127, 0],
+                    np.int16)
+    rows, outs = [], []
+    for i in range(6):
+        soft = vals[ext_rng.integers(0, len(vals), 4 * (768 + 6))] if i else np.full(4 * 774, 32767, np.int16)
+        o = np.zeros(768, np.uint8)
+        r.ref_viterbi(P(soft), 768, P(o))
+        rows.append(soft)
+        outs.append(o)
+    g = dict(np.load(os.path.join(HERE, "viterbi_kat.npz")))
+    g["in_extreme"], g["out_extreme"] = np.stack(rows), np.stack(outs)
+    np.savez_compressed(os.path.join(HERE, "viterbi_kat.npz"), **g)
     print("golden vectors written to", HERE)
 
 

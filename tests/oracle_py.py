@@ -33,6 +33,8 @@ def oracle():
         _o.orc_process_block0.restype = C.c_int16
         _o.orc_rs_dec.restype = C.c_int16
         _o.orc_ofdm_run.argtypes = [C.c_void_p, C.c_int64, C.c_int16, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _o.orc_get_snr.restype = C.c_int16
+        _o.orc_init()           # tables built once: the functions are then safe from threads
     return _o
 
 
@@ -131,3 +133,49 @@ class MP4:
                                   C.byref(nc), C.byref(na), P(aus), P(crc))
         return dict(status=int(st), out=out, n_corrected=int(nc.value), num_aus=int(na.value),
                     au_start=aus, au_crc=crc)
+
+
+def get_snr(spectrum):
+    """get_snr (ofdm-decoder.cpp:212-230) of a cf32[2048] spectrum (float array [4096])"""
+    return int(oracle().orc_get_snr(P(np.ascontiguousarray(spectrum, np.float32))))
+
+
+def fft(x):
+    """the oracle's 2048-point FFT (double precision, rounded to float) of cf32 [4096]"""
+    out = np.zeros(4096, np.float32)
+    oracle().orc_fft2048(P(np.ascontiguousarray(x, np.float32)), P(out), 0)
+    return out
+
+
+def decode_stream(iq, max_frames, subch, method=1, threshold=3):
+    """The reference CPU path restated, over one stream: ofdmProcessor::run (frames,
+    soft bits), ficHandler::process_ficInput per FIC block, dabConcurrent per
+    subchannel (16-CIF de-interleave, UEP/EEP depuncture, Viterbi, energy dispersal).
+    subch: tuples (startAddr, CUs, bitRate, protLevel, uep, ...) with uep = 1 for UEP.
+    Returns dict(n, info, soft [n,75,3072], fic [n,4,768], crc [n,12], msc [4n][nsub][24*maxbr])."""
+    n, info, soft = ofdm_run(iq, max_frames, threshold=threshold, method=method)
+    fic = np.zeros((n, 4, 768), np.uint8)
+    crc = np.zeros((n, 12), np.uint8)
+    for f in range(n):
+        blk = soft[f, 0:3].reshape(-1)
+        for b in range(4):
+            fic[f, b], crc[f, 3 * b:3 * b + 3] = fic_process(blk[2304 * b:2304 * (b + 1)])
+    maxb = 24 * max([sc[2] for sc in subch] + [8])
+    msc = np.zeros((4 * n, len(subch), maxb), np.uint8)
+    cifs = soft[:, 3:75].reshape(4 * n, -1)
+    for k, sc in enumerate(subch):
+        sa, ln, br, pl, uep = sc[:5]
+        frag = np.ascontiguousarray(cifs[:, sa * 64:(sa + ln) * 64])
+        out = np.zeros((4 * n, 24 * br), np.uint8)
+        assert oracle().orc_msc_stream(uep, br, pl, ln * 64, 4 * n, P(frag), P(out)) == 0
+        msc[:, k, :24 * br] = out
+    return dict(n=n, info=info, soft=soft, fic=fic, crc=crc, msc=msc)
+
+
+def decode_streams(iqs, max_frames, subch, method=1, threads=16):
+    """decode_stream over several streams on a thread pool (the oracle is reentrant
+    and ctypes drops the GIL during the calls)"""
+    from concurrent.futures import ThreadPoolExecutor
+    oracle()
+    with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
+        return list(ex.map(lambda x: decode_stream(x, max_frames, subch, method), iqs))

@@ -58,6 +58,8 @@ def test_viterbi_golden(ctx):
         soft = g[f"in_{nb}"]
         want = g[f"out_{nb}"]
         assert np.array_equal(ctx.viterbi(soft, nb), want)
+    # int16 extremes: the reference's int16_t temp = input + 127 wraps (viterbi.cpp:230-233)
+    assert np.array_equal(ctx.viterbi(g["in_extreme"], 768), g["out_extreme"])
 
 
 def test_viterbi_extremes(ctx):
@@ -134,6 +136,21 @@ def test_acs_pairs_mixed_profiles(ctx, seed):
         assert np.array_equal(gpu[i], orc.viterbi(soft[i], nb)), (np_force, "mother", i)
 
 
+def test_every_profile_golden(ctx):
+    """all 60 UEP rows, the unknown-profile fallback, EEP-A 1-4 (incl. 8 kbit/s) and EEP-B
+    1-4 through dabgpu_msc_deconvolve against the reference's uep_/eep_deconvolve output
+    (tests/golden/profiles_kat.npz, deconvolve.cpp:39-366)"""
+    import dabamd
+    g = np.load(os.path.join(GOLD, "profiles_kat.npz"))
+    cases = [tuple(int(x) for x in c) for c in g["cases"]]
+    frags = g["frags"].astype(np.int16)
+    subs = [dabamd.Subch(0, 0, br, pl, uf, 0) for uf, br, pl in cases]
+    outs = ctx.msc_deconvolve(frags, subs)
+    for i, (uf, br, pl) in enumerate(cases):
+        nb = 24 * br
+        assert np.array_equal(np.packbits(outs[i] ^ orc.prbs(nb)), g["out"][i, :nb // 8]), (uf, br, pl)
+
+
 def test_msc_golden(ctx):
     import os
     import dabamd
@@ -181,15 +198,26 @@ def test_prs_sync_matches_oracle(ctx, synth_stream):
     iq.free()
 
 
-def test_block0_matches_oracle(ctx, synth_stream):
-    g, info, _ = synth_stream
+@pytest.mark.parametrize("method", [0, 1, 2])
+@pytest.mark.parametrize("cfo", [0.0, 2700.0, -4200.0])
+def test_block0_matches_oracle(ctx, method, cfo):
+    """processBlock_0 (ofdm-decoder.cpp:85-162): the coarse offset of freqSyncMethod 0/1/2
+    on a block 0 seen through a frequency offset (carriers shifted by a few bins), and
+    get_snr (within 1 dB: the reference sums in bin order, the GPU as a tree)"""
+    from dabamd.synth import Ensemble
+    import dabamd
+    g = Ensemble(4, snr_db=15.0, cfo_hz=cfo).generate(23, truth=False)
+    # block 0 of each frame where the transmitter put it (null, then the PRS's guard)
+    b0s = [g["frame0"] + k * 196608 + 2656 + 504 for k in range(4)]
     iq = ctx.put(g["iq"])
-    frs = _frames_from_oracle(info, len(g['iq']) // 2)
-    corr = ctx.block0(iq, frs)
-    for i, fi in enumerate(info):
-        b0 = fi.window_start + fi.start_index
-        c, _ = orc.process_block0(g["iq"][2 * b0:2 * (b0 + 2048)])
-        assert corr[i] == c
+    frs = [dabamd.Frame(iq_base=0, n_samples=len(g["iq"]) // 2, window=b - 504, block0=b, out_slot=i, flags=1)
+           for i, b in enumerate(b0s)]
+    corr, snr = ctx.block0(iq, frs, method=method, with_snr=True)
+    for i, b0 in enumerate(b0s):
+        blk = g["iq"][2 * b0:2 * (b0 + 2048)]
+        c, _ = orc.process_block0(blk, method=method)
+        assert corr[i] == c, (method, cfo, i, corr[i], c)
+        assert abs(int(snr[i]) - orc.get_snr(orc.fft(blk))) <= 1
     iq.free()
 
 
@@ -329,18 +357,6 @@ def test_pipeline_sample_drop_follows_oracle(ctx):
     assert any(info[k].start_index != info[3].start_index for k in range(5, F * runs))   # the shift was seen
     pipe.close()
     diq.free()
-
-
-def test_pipeline_large_cfo_runs(ctx):
-    """at 2.3 kHz the reference's coarse AFC wanders (startIndex up to ~1900): the pipeline
-    must follow or stop cleanly, never read outside the stream"""
-    import dabamd
-    subch = [(0, 96, 128, 3, 1, 0)]
-    try:
-        _pipeline_decode(ctx, [7], 3, subch, cfo=2300.0, snr=25.0, runs=2)
-    except dabamd.DabError as e:
-        assert "lost sync" in str(e) or "ran out" in str(e)
-    ctx.check()
 
 
 # ---------------------------------------------------------------- DAB+

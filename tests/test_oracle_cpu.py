@@ -47,6 +47,66 @@ def test_msc_deconvolve_matches_reference_fixtures():
         assert np.array_equal(got, want[:nb]), (uf, br, pl)
 
 
+def test_viterbi_int16_extremes_match_reference_fixtures():
+    """viterbi.cpp:230-233 (int16_t temp = input + 127 wraps above 32640)"""
+    g = _g("viterbi_kat.npz")
+    for soft, want in zip(g["in_extreme"], g["out_extreme"]):
+        assert np.array_equal(orc.viterbi(soft, 768), want)
+
+
+def _profile_cases():
+    g = _g("profiles_kat.npz")
+    return g, [tuple(int(x) for x in c) for c in g["cases"]]
+
+
+def test_every_profile_matches_reference_fixtures():
+    """all 60 UEP rows, the unknown-profile fallback, EEP-A 1-4 (incl. 8 kbit/s level 2)
+    and EEP-B 1-4: the oracle's depuncture + Viterbi against the reference's
+    uep_/eep_deconvolve output (deconvolve.cpp:39-366)"""
+    g, cases = _profile_cases()
+    assert sum(1 for c in cases if c[0] == 0) >= 63 and sum(1 for c in cases if c[0] == 1) >= 40
+    for i, (uf, br, pl) in enumerate(cases):
+        nb = 24 * br
+        frag = g["frags"][i, :g["used"][i]].astype(np.int16)
+        got = orc.msc_deconvolve(1 if uf == 0 else 0, br, pl, frag) ^ orc.prbs(nb)
+        assert np.array_equal(np.packbits(got), g["out"][i, :nb // 8]), (uf, br, pl)
+
+
+def test_product_profiles_match_oracle():
+    """the decoder's own depuncturing table (csrc/dab_tables.h, host make_profile) gives the
+    oracle's (L_i, PI_i) segments for every fixture profile -- so the product table is
+    pinned to the reference through the oracle, not only through GPU decodes"""
+    import dabamd
+    g, cases = _profile_cases()
+    for i, (uf, br, pl) in enumerate(cases):
+        nb, frag, segs, fallback = dabamd.subch_profile(dabamd.Subch(0, 0, br, pl, uf, 0))
+        L, PI = np.zeros(4, np.int16), np.zeros(4, np.int16)
+        if uf == 0:
+            found = orc.oracle().orc_uep_profile(br, pl, P(L), P(PI))
+            assert fallback == (found == 0), (br, pl)
+        else:
+            assert orc.oracle().orc_eep_profile(br, pl, P(L), P(PI))
+        want = [(int(L[k]), int(PI[k])) for k in range(4) if L[k] > 0]
+        assert nb == 24 * br and segs == want, (uf, br, pl, segs, want)
+        assert frag == g["used"][i], (uf, br, pl, frag, g["used"][i])
+
+
+def test_product_tables_match_reference_fixtures():
+    """the product's PRS refTable and frequency de-interleaver (host-built, uploaded to
+    the device as they are) against the reference's phasetable/mapper output"""
+    import dabamd
+    g = _g("tables.npz")
+    assert np.array_equal(dabamd.host_table(dabamd.TABLE_PRS), g["ref_table"])
+    assert np.array_equal(dabamd.host_table(dabamd.TABLE_MAPPER), g["mapper"])
+    ra = np.zeros(18, np.float32)
+    ref = g["ref_table"].astype(np.float64)
+    # refArg[i] = arg(ref[i] conj(ref[i+1])) (ofdm-decoder.cpp:71-74), recomputed in float
+    got = dabamd.host_table(dabamd.TABLE_REFARG)
+    z = (g["ref_table"][:18, 0] + 1j * g["ref_table"][:18, 1]).astype(np.complex64) * \
+        np.conj((g["ref_table"][1:19, 0] + 1j * g["ref_table"][1:19, 1]).astype(np.complex64))
+    assert np.allclose(got, np.angle(z).astype(np.float32), atol=1e-6)
+
+
 def test_rs_matches_reference_fixtures():
     g = _g("rs_kat.npz")
     for cw, dec, ret in zip(g["cw"], g["dec"], g["ret"]):
@@ -148,7 +208,7 @@ def test_abi_library_exports_every_declared_symbol():
     lib = dabamd.lib()
     for n in sorted(names):
         assert hasattr(lib, n), n
-    assert lib.dabgpu_abi_version() == 1
+    assert lib.dabgpu_abi_version() == 2
 
 
 def test_abi_fails_loudly_without_device():
