@@ -2,19 +2,30 @@
 
 Workload (config C3): E synthetic Mode-I ensembles per GPU (default 64), each with
 9 UEP-3 128 kbit/s subchannels filling all 864 CUs.  One step decodes F frames
-(default 8) of every ensemble through the full hot path: PRS sync (findIndex),
-block-0 AFC, FFT + DQPSK + frequency de-interleave of 75 symbols, FIC
-depuncture/Viterbi/PRBS/CRC, MSC 16-CIF time de-interleave + UEP depuncture +
-Viterbi + PRBS for every subchannel.  IQ (cf32) is resident in HBM before the
-timed region; the streams were acquired (null search) during warm-up.
+(default 24) of every ensemble through the full hot path: findIndex, block 0,
+FFT + DQPSK + frequency de-interleave of 75 symbols, FIC depuncture/Viterbi/PRBS/
+CRC, MSC 16-CIF time de-interleave + UEP depuncture + Viterbi + PRBS for every
+subchannel.  IQ (cf32) is resident in HBM before the timed region; the streams were
+acquired (null search) during warm-up.  --cfo HZ runs the same workload through a
+carrier frequency offset (the general NCO path: per-sample oscillator indices,
+running coarse/fine AFC).
 
-Multi-GPU: one process per GPU; ensembles are sharded by rank (independent
-streams, no data-path collective -> weak scaling); barrier + max-over-ranks
-timing.  value = symbols decoded by all ranks / max time.
+Multi-GPU (C4): one process per GPU.  `python bench.py --gpus N` starts the N ranks
+itself (torch.distributed.run, 127.0.0.1) unless it already runs under a launcher.
+--iq-source local (default): each rank generates its own ensembles (seeded by rank)
+straight into its HBM -- no data-path collective, weak scaling.  --iq-source rccl:
+rank 0 holds every rank's IQ as int16 (.sdr samples) and scatters each step's chunk
+to the ranks with grouped send/recv over RCCL (xGMI) while they decode the previous
+one; the receivers convert the samples to cf32 on the GPU (dabgpu_iq_convert).  With
+N > 1 the default run also measures that scatter on its own ("stream_split"), so the
+link-bound rate is reported beside the rank-local one.  value = symbols decoded by
+all ranks / max-over-ranks time.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -23,6 +34,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "sdr-j-dab_amd"))
 
+TF, TNULL, TU, TS = 196608, 2656, 2048, 2552
 RT_SYMBOLS = 76 / 0.096            # symbols/s of one real-time Mode-I ensemble (791.67)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
@@ -37,18 +49,34 @@ WORKLOADS = {
 }
 
 
+# ------------------------------------------------------------------ processes
+def launch_ranks(n):
+    """Start n ranks of this command under torch.distributed.run (one process per GPU)
+    and return its exit code.  Called before this process touches the GPU; the ranks
+    are child processes (no exec)."""
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    return subprocess.call(cmd, env=env)
+
+
 def dist_setup(n_gpus):
+    """rank, local rank, world size and the torch.distributed module (None for 1 rank).
+    RCCL ("nccl") when every local rank has its own GPU; gloo when ranks share one (a
+    rehearsal of the N > 1 path on a 1-GPU box) or there is no GPU."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != n_gpus:
+        raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}")
     dist = None
     if world > 1:
         import torch
         import torch.distributed as td
-        # RCCL when every local rank has its own GPU (the driver's 1..8-GPU node runs);
-        # gloo when ranks share one (a rehearsal of the N > 1 path on a 1-GPU box) or
-        # there is no GPU.  The path itself has no collective: only the start/stop
-        # barriers and the max-over-ranks time go through torch.distributed.
         ngpu = torch.cuda.device_count()
         lws = int(os.environ.get("LOCAL_WORLD_SIZE", str(world)))
         backend = os.environ.get("DAB_DIST_BACKEND") or ("nccl" if ngpu >= lws and ngpu > 0 else "gloo")
@@ -89,6 +117,52 @@ def allreduce_max(dist, x):
     return float(t.item())
 
 
+# --------------------------------------------------------------- stream split
+def to_s16(iq):
+    """cf32 IQ -> interleaved int16 as an .sdr recording stores it (x * 32768, rounded,
+    clipped): the receivers' dabgpu_iq_convert(DABGPU_IQ_S16) gives x back to 2^-15"""
+    return np.clip(np.rint(np.asarray(iq, np.float32) * 32768.0), -32768, 32767).astype(np.int16)
+
+
+def chunk_layout(stream_len, F):
+    """samples per stream chunk (F frames) and the number of chunks covering a stream"""
+    cs = F * TF
+    return cs, (stream_len + cs - 1) // cs
+
+
+def scatter_chunk(dist, rank, world, sends, recv):
+    """Stream split: rank 0 sends sends[r] (a tensor) to rank r (r >= 1) as one grouped
+    send/recv (ncclGroupStart/End under RCCL; batched p2p under gloo); ranks >= 1
+    receive into `recv`.  Returns the request list (wait on it)."""
+    import torch.distributed as td
+    staged = td.get_backend() == "gloo" and ((recv is not None and recv.is_cuda) or
+                                             (sends is not None and sends[-1].is_cuda))
+    if staged:
+        # gloo (ranks sharing one GPU: a rehearsal of this path) moves host tensors only
+        ops = []
+        if rank == 0:
+            for r in range(1, world):
+                ops.append(td.P2POp(td.isend, sends[r].cpu(), r))
+            return td.batch_isend_irecv(ops)
+        host = recv.new_empty(recv.shape, device="cpu")
+        reqs = td.batch_isend_irecv([td.P2POp(td.irecv, host, 0)])
+
+        class _Staged:
+            def wait(self):
+                for q in reqs:
+                    q.wait()
+                recv.copy_(host)
+        return [_Staged()]
+    ops = []
+    if rank == 0:
+        for r in range(1, world):
+            ops.append(td.P2POp(td.isend, sends[r], r))
+    else:
+        ops.append(td.P2POp(td.irecv, recv, 0))
+    return td.batch_isend_irecv(ops) if ops else []
+
+
+# ----------------------------------------------------------------- CPU side
 def pmc_traffic(kernel, workload):
     """HBM bytes per full-batch launch of `kernel` from the newest committed PMC
     summary for this workload (profiles/rNN_traffic_<workload>.json, made by
@@ -106,67 +180,129 @@ def pmc_traffic(kernel, workload):
                                    "write_bytes": k["write_bytes"], "source": os.path.basename(files[-1])}
 
 
-def cpu_baseline(frames=2, budget_s=20.0, workers=None, workload="c3"):
-    """Reference CPU path on the host cores: MSC/FIC depuncture+Viterbi through the
-    reference's own compiled viterbi.cpp+spiral-sse.c+deconvolve.cpp (oracle/_ref);
-    OFDM front end through the oracle's C restatement (FFTW3f absent).  One worker
-    per core, each decoding its own synthetic ensemble for a bounded time."""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_cores():
+    """the cores this process may use (the GPU box's CPU share: OMP_NUM_THREADS caps it)"""
+    cores = sorted(os.sched_getaffinity(0))
+    cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return cores[:cap] if cap > 0 else cores
+
+
+def cpu_baseline(frames=2, budget_s=20.0, workload="c3", cfo=0.0):
+    """The reference CPU path on the host cores: one worker process per
+    core, pinned (sched_setaffinity = taskset), each decoding its own synthetic ensemble
+    of the workload for a bounded time.  Stages: OFDM front end = the oracle's C
+    restatement of ofdmProcessor::run/ofdmDecoder (FFTW3f absent: its FFT is a
+    double-precision radix-2 stand-in); FIC = restated depuncture + the reference's
+    viterbi.cpp + spiral-sse.c + check_CRC_bits; MSC = restated 16-CIF de-interleave +
+    the reference's deconvolve.cpp (UEP/EEP + Viterbi) + PRBS; DAB+ = the reference's
+    firecode_checker + reedSolomon inside the restated mp4Processor glue
+    (oracle/ref_wrap.cpp: ref_mp4_add)."""
     import multiprocessing as mp
-    workers = workers or min(16, os.cpu_count() or 1)
+    cores = cpu_cores()
     ctx = mp.get_context("fork")
     q = ctx.Queue()
-    procs = [ctx.Process(target=_cpu_worker, args=(w, frames, budget_s, q, workload)) for w in range(workers)]
+    procs = [ctx.Process(target=_cpu_worker, args=(w, core, frames, budget_s, q, workload, cfo))
+             for w, core in enumerate(cores)]
     for p in procs:
         p.start()
     res = [q.get() for _ in procs]
     for p in procs:
         p.join()
-    syms = sum(r[0] for r in res)
-    secs = max(r[1] for r in res)
-    kind = "reference" if all(r[2] for r in res) else "port"
-    return syms / secs, workers, kind, syms
+    secs = max(r["secs"] for r in res)
+    tot = {k: sum(r[k] for r in res) for k in ("symbols", "fic_bits", "msc_bits", "rs_cw", "t_ofdm", "t_fic",
+                                               "t_msc", "t_dabplus")}
+    kind = "reference" if all(r["ref"] for r in res) else "port"
+    return dict(value=tot["symbols"] / secs, cores=len(cores), kind=kind, tot=tot, secs=secs,
+                nproc=os.cpu_count(), cpu=cpu_model())
 
 
-def _cpu_worker(w, frames, budget_s, q, workload="c3"):
+def _cpu_worker(w, core, frames, budget_s, q, workload, cfo):
+    os.sched_setaffinity(0, {core})
     sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import ctypes as C
     import oracle_py as orc
     from dabamd.synth import Ensemble
     ref = orc.ref()
     subch = WORKLOADS[workload][0]
-    e = Ensemble(frames + 4, subch=subch, snr_db=300.0)
+    e = Ensemble(frames + 4, subch=subch, snr_db=30.0, cfo_hz=cfo)
     g = e.generate(9000 + w, truth=False)
-    prbs = orc.prbs(3072)
+    prbs = orc.prbs(24 * 384)
+    P = orc.P
+    st = dict(symbols=0, fic_bits=0, msc_bits=0, rs_cw=0, t_ofdm=0.0, t_fic=0.0, t_msc=0.0, t_dabplus=0.0)
+
+    class Mp4(C.Structure):
+        _fields_ = [("bitRate", C.c_int), ("fill", C.c_int), ("blocks", C.c_int), ("ring", C.c_uint8 * (120 * 48))]
+
+    delay = np.array([orc.oracle().orc_interleave_delay(i) for i in range(16)])
+    crc_fn = ref.ref_check_crc_bits if ref is not None else orc.oracle().orc_check_crc_bits
     t0 = time.perf_counter()
-    done = 0
     while True:
+        a = time.perf_counter()
         n, info, soft = orc.ofdm_run(g["iq"], frames + 4)
-        cifs = soft[:, 3:75].reshape(4 * n, -1)
-        for f in range(n):
+        b = time.perf_counter()
+        st["t_ofdm"] += b - a
+        for f in range(n):                               # ficHandler: 4 blocks per frame
             fic = soft[f, 0:3].reshape(-1)
-            for b in range(4):
-                orc.fic_process(fic[2304 * b:2304 * (b + 1)])
-        mp4 = [orc.MP4(sc[2]) if sc[5] else None for sc in subch]
-        for c in range(4 * n):
-            for k, (sa, ln, br, pl, uep, dp) in enumerate(subch):
-                frag = np.ascontiguousarray(cifs[c, sa * 64:(sa + ln) * 64])
+            for blk in range(4):
+                vb = np.zeros(3096, np.int16)
+                orc.oracle().orc_fic_depuncture(P(np.ascontiguousarray(fic[2304 * blk:2304 * (blk + 1)])), P(vb))
+                bits = np.zeros(768, np.uint8)
+                if ref is not None:
+                    ref.ref_viterbi(P(vb), 768, P(bits))
+                else:
+                    orc.oracle().orc_viterbi(P(vb), 768, P(bits))
+                bits ^= prbs[:768]
+                for k in range(3):
+                    crc_fn(P(bits[256 * k:]), 256)
+                st["fic_bits"] += 768
+        c = time.perf_counter()
+        st["t_fic"] += c - b
+        cifs = soft[:, 3:75].reshape(4 * n, -1)
+        mp4 = [Mp4(sc[2], 0, 0) if sc[5] else None for sc in subch]
+        tm = 0.0
+        for k, (sa, ln, br, pl, uep, dp) in enumerate(subch):
+            frags = cifs[:, sa * 64:(sa + ln) * 64]
+            idx = np.arange(ln * 64)
+            d = delay[idx & 15]
+            for cc in range(16, 4 * n):                   # dabConcurrent: 16-CIF de-interleave
+                frag = np.ascontiguousarray(frags[cc - d, idx])
                 out = np.zeros(24 * br, np.uint8)
                 if ref is not None:
-                    if uep:
-                        ref.ref_uep_deconvolve(br, pl, orc.P(frag), len(frag), orc.P(out))
-                    else:
-                        ref.ref_eep_deconvolve(br, pl, orc.P(frag), len(frag), orc.P(out))
+                    fn = ref.ref_uep_deconvolve if uep else ref.ref_eep_deconvolve
+                    fn(br, pl, P(frag), len(frag), P(out))
                     out ^= prbs[:24 * br]
                 else:
                     out = orc.msc_deconvolve(uep, br, pl, frag)
+                st["msc_bits"] += 24 * br
                 if mp4[k] is not None:
-                    mp4[k].add(out)
-        done += n * 76
+                    t1 = time.perf_counter()
+                    nok = C.c_int()
+                    if ref is not None and ref.ref_mp4_add(C.byref(mp4[k]), P(out), C.byref(nok)) == 3:
+                        st["rs_cw"] += br // 8
+                    tm += time.perf_counter() - t1
+        dd = time.perf_counter()
+        st["t_msc"] += dd - c - tm
+        st["t_dabplus"] += tm
+        st["symbols"] += n * 76
         el = time.perf_counter() - t0
         if el >= budget_s:
             break
-    q.put((done, el, ref is not None))
+    st["secs"] = el
+    st["ref"] = ref is not None
+    q.put(st)
 
 
+# ----------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -177,50 +313,124 @@ def main():
     ap.add_argument("--frames", type=int, default=24,
                     help="frames per ensemble per step (the pipeline's batch: 24 frames = 2.3 s of air time; "
                          "throughput saturates from ~24 on MI355X, profiles/r01_frames_sweep.txt)")
+    ap.add_argument("--cfo", type=float, default=0.0, help="carrier frequency offset of the synthetic IQ (Hz)")
+    ap.add_argument("--iq-source", choices=["local", "rccl"], default="local")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
     rank, local, world, dist = dist_setup(args.gpus)
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         # before this process touches the GPU: the workers are forked children
-        cpu = cpu_baseline(budget_s=args.cpu_seconds, workload=args.workload)
+        cpu = cpu_baseline(budget_s=args.cpu_seconds, workload=args.workload, cfo=args.cfo)
     import dabamd
     from dabamd.synth import Ensemble
 
     SUBCH, E_default, wl_desc = WORKLOADS[args.workload]
     dabplus = any(s[5] for s in SUBCH)
     E, F = args.ensembles or E_default, args.frames
-    total_frames = F * (args.warmup + args.steps + 1) + 1   # +1 step: the profiled pass
-    ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0)
+    total_frames = F * (args.warmup + args.steps + 1) + 1   # +1 step: the checked pass
+    ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0, cfo_hz=args.cfo)
     ctx = dabamd.Context(rank_device(local))
     stride = ens.length
-    # generated in groups straight into HBM: host memory stays at one group (~2 GB)
-    # however many ensembles and frames the run decodes
+    rccl = args.iq_source == "rccl" and world > 1
+    # IQ generated in groups straight into HBM: host memory stays at one group however
+    # many ensembles and frames the run decodes.  Ensemble 0 of rank 0 is generated with
+    # its transmitted bits (the checked step compares the decoded MSC/FIC bits with them).
     t0 = time.time()
     diq = ctx.buf(E * 2 * stride * 4)
+    truth = None
+    seed0 = rank_seed0(0 if rccl else rank, E)
+    cs, nchunks = chunk_layout(stride, F)
+    src16 = None
+    if rccl and rank == 0:
+        import torch
+        # rank 0's pool as int16, chunk-major [chunk][ensemble][2*cs]: chunk k of every
+        # stream is one contiguous message per destination rank
+        src16 = torch.zeros((nchunks, E, 2 * cs), dtype=torch.int16, device=f"cuda:{rank_device(local)}")
     group = 8
-    for g0 in range(0, E, group):
-        n = min(group, E - g0)
-        part = ens.generate_many(n, seed0=rank_seed0(rank, E) + g0, threads=min(16, os.cpu_count() or 1))
-        diq.upload_at(part, g0 * 2 * stride * 4)
-        del part
+    if rank == 0 or not rccl:
+        for g0 in range(0, E, group):
+            n = min(group, E - g0)
+            if g0 == 0 and rank == 0:
+                import threading
+                box = {}
+                th = threading.Thread(target=lambda: box.update(g=ens.generate(seed0, truth=True)))
+                th.start()
+                rest = ens.generate_many(n - 1, seed0=seed0 + 1, threads=min(16, os.cpu_count() or 1))
+                th.join()
+                truth = box["g"]
+                part = np.concatenate([truth["iq"][None, :], rest])
+                del rest
+            else:
+                part = ens.generate_many(n, seed0=seed0 + g0, threads=min(16, os.cpu_count() or 1))
+            if src16 is not None:
+                p16 = np.zeros((n, nchunks * 2 * cs), np.int16)
+                p16[:, :2 * stride] = to_s16(part)
+                src16[:, g0:g0 + n] = torch.from_numpy(p16.reshape(n, nchunks, 2 * cs).transpose(1, 0, 2).copy()).to(
+                    src16.device)
+                part = p16[:, :2 * stride].astype(np.float32) / 32768.0   # what the receivers decode
+                del p16
+            diq.upload_at(part, g0 * 2 * stride * 4)
+            del part
     gen_s = time.time() - t0
     subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, dabamd.SUBCH_DABPLUS if s[5] else 0)
             for s in SUBCH]
     pipe = dabamd.Pipeline(ctx, E, F, subs)
-    pipe.acquire(diq, stride, [0] * E, [stride] * E)
-    n_avail = [stride] * E
 
-    def step(download=False):
-        r = pipe.run(diq, stride, n_avail, download=download)
-        if dabplus:
-            return r, pipe.dabplus(download=download)
-        return r, None
+    # stream split over RCCL: chunk k of every stream from rank 0 to each rank
+    feed = None
+    if rccl:
+        import torch
+        dev = f"cuda:{rank_device(local)}"
+        recv = torch.zeros((E, 2 * cs), dtype=torch.int16, device=dev) if rank else None
+        got = [0]                                         # chunks available on this rank
 
-    for _ in range(args.warmup):
-        step()
+        def feed_begin(k):
+            """start moving chunk k of every stream from rank 0 to each rank"""
+            if k >= nchunks:
+                return None
+            return scatter_chunk(dist, rank, world, [src16[k]] * world if rank == 0 else None, recv)
+
+        def feed_end(k, reqs):
+            """wait for chunk k and convert it into this rank's cf32 stream buffer"""
+            if reqs is None:
+                return
+            for r in reqs:
+                r.wait()
+            if rank:
+                torch.cuda.current_stream().synchronize()
+                m = min(cs, stride - k * cs)
+                for e in range(E):
+                    ctx.iq_convert(dabamd.IQ_S16, _TorchBuf(recv[e]), m, diq,
+                                   dst_off=(e * 2 * stride + 2 * k * cs) * 4)
+                ctx.sync()                                # recv is reused by the next chunk
+            got[0] = k + 1
+        feed = (feed_begin, feed_end)
+        for k in range(2):
+            feed_end(k, feed_begin(k))
+
+    def avail():
+        if not rccl:
+            return [stride] * E
+        return [min(stride, got[0] * cs)] * E
+
+    pipe.acquire(diq, stride, [0] * E, avail())
+
+    def step(k, download=False):
+        # chunk k + 2 travels while step k decodes (the frames of step k need chunks <= k + 1)
+        reqs = feed[0](k + 2) if feed is not None else None
+        r = pipe.run(diq, stride, avail(), download=download)
+        d = pipe.dabplus(download=download) if dabplus else None
+        if feed is not None:
+            feed[1](k + 2, reqs)
+        return r, d
+
+    for i in range(args.warmup):
+        step(i)
     pipe.sync()
     # per-kernel HIP events on each launch's stream over the timed steps (recording
     # adds no synchronisation); summed and counted by the pipeline
@@ -228,8 +438,8 @@ def main():
     barrier(dist)
     pipe.sync()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
+    for i in range(args.steps):
+        step(args.warmup + i)
     pipe.sync()
     el = time.perf_counter() - t0
     barrier(dist)
@@ -239,9 +449,30 @@ def main():
     # kernel time per step and per launch over the timed region
     tm = {k: (v[0] / args.steps, v[0] / max(v[1], 1)) for k, v in tsum.items()}
 
-    # one extra step (outside the timed region) whose outputs are checked
-    (fic, crc, msc, valid), dp = step(download=True)
-    crc_ok = float(crc.mean())
+    # one extra step (outside the timed region) whose outputs are checked against the
+    # transmitted bits of ensemble 0 (rank 0): every FIB CRC, every MSC subchannel
+    ck = args.warmup + args.steps
+    st0 = pipe.state(0)
+    (fic, crc, msc, valid), dp = step(ck, download=True)
+    check = None
+    if rank == 0 and truth is not None:
+        st1 = pipe.state(0)
+        f0 = st1.frames_run
+        cif0 = st0.cif_count
+        g_frame0 = (cif0 // 4)
+        flip = _crc_flip()
+        fic_ok = all(np.array_equal(fic[0, f, b] ^ flip, truth["fic"][g_frame0 + f, b])
+                     for f in range(f0) for b in range(4))
+        msc_ok = msc_n = 0
+        for c in range(4 * f0):
+            if not valid[0, c]:
+                continue
+            for k, sc in enumerate(SUBCH):
+                nb = 24 * sc[2]
+                msc_n += 1
+                msc_ok += int(np.array_equal(msc[0, c, k, :nb], truth["msc"][cif0 + c, k, :nb]))
+        check = {"ensemble": 0, "frames": int(f0), "fic_blocks_equal_transmitted": bool(fic_ok),
+                 "fic_crc_pass_rate": float(crc.mean()), "msc_codewords": msc_n, "msc_equal_transmitted": msc_ok}
     sf_ok = None
     if dp is not None:
         info = dp[0]
@@ -251,6 +482,12 @@ def main():
 
     symbols = world * E * F * 76 * args.steps
     value = symbols / el
+    split = None
+    if world > 1 and not rccl:
+        try:
+            split = stream_split_probe(dist, rank, world, local, E, F)
+        except Exception as e:                          # never costs the main measurement
+            split = {"error": repr(e)[:300]}
     if rank != 0:
         return
     # dominant kernel + its roofline
@@ -262,15 +499,19 @@ def main():
     acs_ms = max(tm[acs_stage][1], 1e-9)            # average launch duration
     acs_ops = acs_steps * 64 * 4                    # 2 adds + compare + select per ACS
     demod_ms = max(tm["demod"][1], 1e-9)
-    demod_bytes = E * F * 75 * (8 * 2552 + 2 * 3072)
-    roof_valu = {"kernel": f"{acs_kernel[5:]} (Viterbi ACS)", "bound": "valu", "achieved": acs_ops / (acs_ms * 1e-3) / 1e12,
-                 "peak": VALU_PEAK_TOPS, "unit": "TOP/s", "traffic": pmc_traffic(acs_kernel, args.workload),
-                 "note": "4 int ops per add-compare-select x 64 states per trellis step; peak = 256 CU x 4 SIMD x 32 lanes x 2.4 GHz"}
+    demod_bytes = E * F * (75 * (8 * TS + 2 * 3072) + 8 * TU)   # + the findIndex window
+    demod_kernel = "dab::k_demod_wg<true, true>" if args.cfo else "dab::k_demod_wg<false, true>"
+    roof_valu = {"kernel": f"{acs_kernel[5:]} (Viterbi ACS)", "bound": "valu",
+                 "achieved": acs_ops / (acs_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
+                 "traffic": pmc_traffic(acs_kernel, args.workload),
+                 "note": "4 int ops per add-compare-select x 64 states per trellis step; peak = 256 CU x 4 SIMD x "
+                         "32 lanes x 2.4 GHz"}
     roof_valu["frac"] = roof_valu["achieved"] / roof_valu["peak"]
-    roof_hbm = {"kernel": "k_demod_wg (FFT+DQPSK)", "bound": "hbm",
+    roof_hbm = {"kernel": f"{demod_kernel[5:]} (findIndex + FFT + DQPSK)", "bound": "hbm",
                 "achieved": demod_bytes / (demod_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "traffic": pmc_traffic("dab::k_demod_wg<false>", args.workload), "algorithmic_bytes": demod_bytes,
-                "note": "algorithmic bytes: 8*T_s cf32 in + 2*2K int16 out per data symbol"}
+                "traffic": pmc_traffic(demod_kernel, args.workload), "algorithmic_bytes": demod_bytes,
+                "note": "algorithmic bytes: 8*T_s cf32 in + 2*2K int16 out per data symbol + 8*T_u of the "
+                        "findIndex window per frame"}
     roof_hbm["frac"] = roof_hbm["achieved"] / roof_hbm["peak"]
     roofline = roof_valu if dom in ("msc_acs", "fic") else roof_hbm
 
@@ -278,29 +519,88 @@ def main():
         "metric": "DAB Mode-I symbols/sec (and real-time ensembles/GPU) at 1/2/4/8 MI355X",
         "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32+u32",
-        "data": "synthetic (dabsynth transmitter, 30 dB SNR)",
-        "config": {"workload": wl_desc,
-                   "ensembles_per_gpu": E, "frames_per_step": F, "parallelism": f"ensemble-shard x{world}"},
+        "vs_baseline": None, "dtype": "f32 (OFDM) + u16x2 packed path metrics (Viterbi, exact)",
+        "data": f"synthetic (dabsynth transmitter, 30 dB SNR, CFO {args.cfo:g} Hz)"
+                + (", int16 .sdr samples scattered from rank 0 over RCCL" if rccl else ""),
+        "config": {"workload": wl_desc, "ensembles_per_gpu": E, "frames_per_step": F,
+                   "parallelism": f"ensemble-shard x{world}", "iq_source": "rccl-scatter" if rccl else "rank-local",
+                   "cfo_hz": args.cfo},
         "realtime_ensembles_per_gpu": value / world / RT_SYMBOLS,
         "roofline": roofline,
         "roofline_hbm_demod": roof_hbm,
         "kernel_ms_per_step": {k: v[0] for k, v in tm.items()},
         "kernel_ms_per_launch": {k: v[1] for k, v in tm.items()},
         "kernel_timing": "HIP events on each launch's stream over the timed steps (rocprofv3 --kernel-trace agrees)",
-        "fic_crc_pass_rate": crc_ok,
+        "checked_step": check,
         "dabplus_last_step": sf_ok,
         "gen_seconds": gen_s,
     }
+    if split is not None:
+        out["stream_split"] = split
     if cpu is not None:
-        v, cores, kind, syms = cpu
-        out["cpu_baseline"] = {"value": v, "unit": "symbols/s", "cores": cores, "kind": kind,
-                               "sample": f"{cores} workers x own synthetic {args.workload.upper()} ensemble "
-                                         f"(6 frames, {len(SUBCH)} subch), ~{args.cpu_seconds:.0f}s each, {syms} "
-                                         "symbols total; Viterbi/depuncture = reference viterbi.cpp+spiral-sse.c+"
-                                         "deconvolve.cpp, OFDM (and DAB+ RS/superframe) = oracle C restatement "
-                                         "(FFTW3f absent)"}
+        t = cpu["tot"]
+        out["cpu_baseline"] = {
+            "value": cpu["value"], "unit": "symbols/s", "cores": cpu["cores"], "kind": cpu["kind"],
+            "sample": f"{cpu['cores']} workers pinned one per core (of nproc {cpu['nproc']}, {cpu['cpu']}), each "
+                      f"its own synthetic {args.workload.upper()} ensemble (6 frames, {len(SUBCH)} subch) for "
+                      f"~{args.cpu_seconds:.0f}s: {t['symbols']} symbols.  FIC/MSC Viterbi + depuncture = reference "
+                      "viterbi.cpp+spiral-sse.c+deconvolve.cpp, DAB+ = reference reed-solomon.cpp+"
+                      "firecode-checker.cpp; OFDM = oracle C restatement (FFTW3f absent: double radix-2 FFT "
+                      "stand-in)",
+            "stages_cpu_seconds": {"ofdm": t["t_ofdm"], "fic": t["t_fic"], "msc": t["t_msc"],
+                                   "dabplus": t["t_dabplus"]},
+            "decoded_mbit_per_s": (t["fic_bits"] + t["msc_bits"]) / cpu["secs"] / 1e6,
+            "rs_codewords_per_s": t["rs_cw"] / cpu["secs"],
+            "realtime_ensembles": cpu["value"] / RT_SYMBOLS,
+        }
     print(json.dumps(out))
+
+
+def _crc_flip():
+    """the FIC output carries each FIB's CRC field inverted, as check_CRC_bits leaves it
+    (dab-constants.h:316-317): xor-ing this restores the transmitted bits"""
+    m = np.zeros(768, np.uint8)
+    for q in range(3):
+        m[256 * q + 240:256 * q + 256] = 1
+    return m
+
+
+class _TorchBuf:
+    """a torch tensor's device memory seen as a dabamd buffer (same device and process)"""
+
+    def __init__(self, t):
+        import ctypes as C
+        self.ptr = C.c_void_p(t.data_ptr())
+
+
+def stream_split_probe(dist, rank, world, local, E, F, reps=3):
+    """Time the C4 stream split on its own: rank 0 sends one step's int16 IQ chunk
+    (E streams x F frames, 4 B per sample) to every other rank in one grouped
+    send/recv; link-bound symbols/s = what the ranks could decode if fed this way."""
+    import torch
+    if dist.get_backend() != "nccl":
+        return None
+    dev = f"cuda:{rank_device(local)}"
+    cs = F * TF
+    buf = torch.ones((E, 2 * cs), dtype=torch.int16, device=dev)
+    ts = []
+    for i in range(reps + 1):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for r in scatter_chunk(dist, rank, world, [buf] * world if rank == 0 else None, buf):
+            r.wait()
+        torch.cuda.synchronize()
+        dist.barrier()
+        if i:
+            ts.append(allreduce_max(dist, time.perf_counter() - t0))
+    t = min(ts)
+    nbytes = buf.numel() * 2
+    return {"bytes_per_rank_per_step": nbytes, "seconds_per_step": t,
+            "GBps_out_of_rank0": (world - 1) * nbytes / t / 1e9, "GBps_per_destination": nbytes / t / 1e9,
+            "link_bound_symbols_per_s": world * E * F * 76 / t,
+            "note": "one step's int16 IQ for every rank from rank 0, grouped send/recv over RCCL (xGMI); the "
+                    "decode is not overlapped here -- see --iq-source rccl for the fed end-to-end rate"}
 
 
 if __name__ == "__main__":

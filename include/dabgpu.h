@@ -174,6 +174,17 @@ int dabgpu_block0(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames
 int dabgpu_ofdm_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n,
                       int16_t *softbits_d, float *softf_d, float *freqcorr_d);
 
+/* The north-star fused front end, one workgroup per frame (k_demod_wg<.., SYNC>):
+ * findIndex on the frame's T_u window (phasereference.cpp:60-88, threshold `level`;
+ * start_index_d[i] as dabgpu_prs_sync), the frame placed at block0 = window +
+ * startIndex with lp_data following getSamples (ofdm-processor.cpp:344-368),
+ * get_snr of block 0 (snr_d, optional, ofdm-decoder.cpp:93) and processToken x 75
+ * as dabgpu_ofdm_demod.  frames[i].block0 / lp_data are ignored; a frame whose
+ * findIndex fails or whose symbols lie past n_samples is skipped (no soft bits). */
+int dabgpu_ofdm_sync_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n, int16_t level,
+                           int32_t *start_index_d, int16_t *snr_d, int16_t *softbits_d, float *softf_d,
+                           float *freqcorr_d);
+
 /* ---- channel decoding (L4) -------------------------------------------- */
 
 /* viterbi::deconvolve batched (viterbi.cpp:225-242): n_cw codewords of

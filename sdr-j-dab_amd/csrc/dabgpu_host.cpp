@@ -525,6 +525,21 @@ int dabgpu_ofdm_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, in
     if (!c || !iq || !fr || !soft || n < 0) return fail(DABGPU_E_ARG, "bad args");
     return demod_impl(c, iq, fr, n, soft, softf, fc, true);
 }
+int dabgpu_ofdm_sync_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t level, int32_t *si,
+                           int16_t *snr, int16_t *soft, float *softf, float *fc) {
+    if (!c || !iq || !fr || !si || !soft || n < 0) return fail(DABGPU_E_ARG, "bad args");
+    void *part = nullptr;
+    const int kChunks = demod_chunks(n, 2);
+    int rc = scratch(c, SC_FC, sizeof(float2) * (size_t)n * kChunks, &part);
+    if (rc) return rc;
+    DemodAux aux{};
+    aux.si = si;
+    aux.snr = snr;
+    aux.level = level;
+    HIPCHK(launch_demod(c->stream, iq, fr, n, kChunks, c->T, soft, softf, (float *)part, true, aux));
+    if (fc) HIPCHK(launch_fc_reduce(c->stream, (const float *)part, kChunks, n, fc));
+    return 0;
+}
 
 // ---- Viterbi operators -------------------------------------------------------
 static int run_viterbi(dabgpu_ctx *c, VitJob &J, int max_nbits) {

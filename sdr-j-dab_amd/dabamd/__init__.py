@@ -15,7 +15,7 @@ import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _PKG = os.path.dirname(_HERE)
-LIB_PATH = os.path.join(_PKG, "lib", "libdabgpu.so")
+LIB_PATH = os.environ.get("DABGPU_LIB") or os.path.join(_PKG, "lib", "libdabgpu.so")   # env: A/B of builds (tools/)
 SYNTH_PATH = os.path.join(_PKG, "lib", "libdabsynth.so")
 
 TU, TS, TG, TNULL, TF, K, L = 2048, 2552, 504, 2656, 196608, 1536, 76
@@ -101,6 +101,7 @@ def lib() -> C.CDLL:
             "dabgpu_prs_sync": ([vp, vp, vp, i32, C.c_int16, vp, vp, vp], i32),
             "dabgpu_block0": ([vp, vp, vp, i32, i32, vp, vp], i32),
             "dabgpu_ofdm_demod": ([vp, vp, vp, i32, vp, vp, vp], i32),
+            "dabgpu_ofdm_sync_demod": ([vp, vp, vp, i32, C.c_int16, vp, vp, vp, vp, vp], i32),
             "dabgpu_viterbi": ([vp, vp, i32, i32, vp], i32),
             "dabgpu_fic_decode": ([vp, vp, i32, vp, vp], i32),
             "dabgpu_fic_decode_frames": ([vp, vp, vp, i32, vp, vp], i32),
@@ -420,6 +421,33 @@ class Context:
             return soft, softf, fc[:, 0] + 1j * fc[:, 1]
         finally:
             for b in (dfr, ds, df, dfc):
+                if b is not None:
+                    b.free()
+
+
+    def sync_demod(self, iq: DevBuf, frames: Sequence[Frame], level: int = 3, with_float: bool = False):
+        """findIndex + get_snr + processToken x 75 in one launch (dabgpu_ofdm_sync_demod).
+        Frame i must have out_slot == i.  Returns (start_index [n], snr [n], ibits [n,75,3072],
+        softf or None, freqcorr [n] complex)."""
+        n = len(frames)
+        fa = (Frame * n)(*frames)
+        dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
+        dsi, dsn = self.buf(4 * n), self.buf(2 * n)
+        ds = self.buf(2 * n * NSYM * SYMBITS)
+        df = self.buf(4 * n * NSYM * SYMBITS) if with_float else None
+        dfc = self.buf(8 * n)
+        try:
+            _chk(lib().dabgpu_ofdm_sync_demod(self.h, iq.ptr, dfr.ptr, n, level, dsi.ptr, dsn.ptr, ds.ptr,
+                                              df.ptr if df else None, dfc.ptr), "ofdm_sync_demod")
+            si = dsi.download(np.int32, n)
+            snr = dsn.download(np.int16, n)
+            soft = ds.download(np.int16, (n, NSYM, SYMBITS))
+            softf = df.download(np.float32, (n, NSYM, SYMBITS)) if df else None
+            fc = dfc.download(np.float32, (n, 2))
+            self.check()
+            return si, snr, soft, softf, fc[:, 0] + 1j * fc[:, 1]
+        finally:
+            for b in (dfr, dsi, dsn, ds, df, dfc):
                 if b is not None:
                     b.free()
 

@@ -108,10 +108,13 @@ def test_pipeline_dropout_reacquires_like_reference(ctx):
     iq = g["iq"].reshape(-1, 2).copy()
     a = g["frame0"] + 3 * 196608 + 40000
     b = a + 300000
+    # (plus a noise floor 20 dB below it: without one, the FFT bins next to the carrier
+    # hold only rounding noise and the soft bits of the half-jammed frame are arbitrary)
     level = float(np.sqrt((iq[:200000] ** 2).sum(1).mean()))
     ph = 2 * np.pi * 100e3 / 2048000 * np.arange(b - a)
-    iq[a:b, 0] = level * np.cos(ph)
-    iq[a:b, 1] = level * np.sin(ph)
+    rng = np.random.default_rng(5)
+    iq[a:b, 0] = level * np.cos(ph) + rng.normal(0, level / 10, b - a)
+    iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
     iq = np.ascontiguousarray(iq.reshape(-1))
     ref = orc.decode_stream(iq, F * runs, sub)
     gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,))
