@@ -129,6 +129,8 @@ int         dabgpu_free(dabgpu_ctx *ctx, void *dptr);
 int         dabgpu_memcpy_h2d(dabgpu_ctx *ctx, void *dst_d, const void *src_h, size_t bytes);
 int         dabgpu_memcpy_d2h(dabgpu_ctx *ctx, void *dst_h, const void *src_d, size_t bytes);
 int         dabgpu_memset_d(dabgpu_ctx *ctx, void *dst_d, int value, size_t bytes);
+/* device-to-device copy on the context stream (asynchronous; regions must not overlap) */
+int         dabgpu_memcpy_d2d(dabgpu_ctx *ctx, void *dst_d, const void *src_d, size_t bytes);
 /* HIP events on the context stream, for timing (ms between two marks) */
 int         dabgpu_event_record(dabgpu_ctx *ctx, int slot);
 /* device-side bounds violations flagged by kernels since the last call (syncs; clears) */
@@ -184,6 +186,13 @@ int dabgpu_ofdm_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *fr
 int dabgpu_ofdm_sync_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n, int16_t level,
                            int32_t *start_index_d, int16_t *snr_d, int16_t *softbits_d, float *softf_d,
                            float *freqcorr_d);
+
+/* One symbol at a time (the reference's ofdmDecoder call pattern, ofdm-decoder.cpp:
+ * 85-190), samples already mixed by the caller: kind 0 = block 0 (samples_d holds
+ * T_u samples; its spectrum becomes the phase reference), kind 1 = a data symbol
+ * (T_s samples; ibits_d[3072] = processToken's soft bits against the stored
+ * spectrum, which then becomes this symbol's).  spectrum_d: cf32[2048] state. */
+int dabgpu_ofdm_symbol(dabgpu_ctx *ctx, const float *samples_d, int kind, float *spectrum_d, int16_t *ibits_d);
 
 /* ---- channel decoding (L4) -------------------------------------------- */
 

@@ -135,6 +135,7 @@ hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
                         const DemodAux &aux);
+hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmTables &T, float *spec, int16_t *ibits);
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
 hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
                           AcqResult *res);

@@ -436,6 +436,11 @@ int dabgpu_memcpy_d2h(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
+int dabgpu_memcpy_d2d(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
+    if (!c) return fail(DABGPU_E_ARG, "null ctx");
+    HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
+    return 0;
+}
 int dabgpu_iq_convert(dabgpu_ctx *c, int format, const void *src, int64_t n_pairs, float *iq) {
     if (!c || (!src && n_pairs > 0) || (!iq && n_pairs > 0) || n_pairs < 0) return fail(DABGPU_E_ARG, "bad args");
     if (format != DABGPU_IQ_U8 && format != DABGPU_IQ_S16) return fail(DABGPU_E_ARG, "unknown IQ format %d", format);
@@ -524,6 +529,11 @@ int dabgpu_ofdm_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, in
                       float *fc) {
     if (!c || !iq || !fr || !soft || n < 0) return fail(DABGPU_E_ARG, "bad args");
     return demod_impl(c, iq, fr, n, soft, softf, fc, true);
+}
+int dabgpu_ofdm_symbol(dabgpu_ctx *c, const float *smp, int kind, float *spec, int16_t *ibits) {
+    if (!c || !smp || !spec || (kind != 0 && kind != 1) || (kind == 1 && !ibits)) return fail(DABGPU_E_ARG, "bad args");
+    HIPCHK(launch_symbol(c->stream, smp, kind, c->T, spec, ibits));
+    return 0;
 }
 int dabgpu_ofdm_sync_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t level, int32_t *si,
                            int16_t *snr, int16_t *soft, float *softf, float *fc) {

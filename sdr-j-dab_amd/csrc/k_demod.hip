@@ -612,6 +612,47 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
     }
 }
 
+// One OFDM symbol at a time, for the single-symbol ofdmDecoder interface
+// (ofdm-decoder.cpp:85-190): kind 0 = block 0 (FFT of samples[0, T_u), the spectrum
+// becomes the phase reference), kind 1 = a data symbol (FFT of samples[T_g, T_s),
+// DQPSK against the stored spectrum -> ibits[3072], spectrum := this symbol's).  The
+// samples are already NCO-mixed by the caller (ofdmProcessor::getSamples); spec holds
+// the previous spectrum in natural bin order.  One workgroup.
+__global__ __launch_bounds__(DT) void k_symbol_wg(const float2 *__restrict__ smp, int kind, OfdmTables T,
+                                                  float2 *__restrict__ spec, int16_t *__restrict__ ibits) {
+    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ TwLds twl;
+    const int t = threadIdx.x;
+    const DemodTw tw = tw_setup(twl, T, t);
+    __syncthreads();
+    const float2 *x = smp + (kind ? TG : 0);
+    float2 a[8];
+#pragma unroll
+    for (int m = 0; m < 8; m++) a[m] = x[t + 256 * m];
+    fft2048_wg(a, ex, tw, t);
+    const int b0 = bin0_of(t);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const int b = b0 + 64 * k;
+        if (kind) {
+            const int c = T.carrier_of_bin[b];
+            if (c >= 0) {
+                const float2 r1 = cmul_conj_exact(a[k], spec[b]);
+                int ir, ii;
+                soft_pair(r1, fabsf(r1.x) + fabsf(r1.y), ir, ii);
+                ibits[c] = (int16_t)ir;
+                ibits[K + c] = (int16_t)ii;
+            }
+        }
+        spec[b] = a[k];
+    }
+}
+
+hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmTables &T, float *spec, int16_t *ibits) {
+    hipLaunchKernelGGL(k_symbol_wg, dim3(1), dim3(DT), 0, st, (const float2 *)smp, kind, T, (float2 *)spec, ibits);
+    return hipGetLastError();
+}
+
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
                         const DemodAux &aux) {

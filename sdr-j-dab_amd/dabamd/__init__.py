@@ -94,6 +94,8 @@ def lib() -> C.CDLL:
             "dabgpu_alloc": ([vp, sz, C.POINTER(vp)], i32), "dabgpu_free": ([vp, vp], i32),
             "dabgpu_memcpy_h2d": ([vp, vp, vp, sz], i32), "dabgpu_memcpy_d2h": ([vp, vp, vp, sz], i32),
             "dabgpu_memset_d": ([vp, vp, i32, sz], i32),
+            "dabgpu_memcpy_d2d": ([vp, vp, vp, sz], i32),
+            "dabgpu_ofdm_symbol": ([vp, vp, i32, vp, vp], i32),
             "dabgpu_iq_convert": ([vp, i32, vp, i64, vp], i32),
             "dabgpu_event_record": ([vp, i32], i32),
             "dabgpu_kernel_errors": ([vp], i32),

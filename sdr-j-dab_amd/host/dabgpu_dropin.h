@@ -21,11 +21,44 @@
 #include <stdexcept>
 #include <vector>
 
+#include <atomic>
+#include <cstdio>
+#include <memory>
+#include <mutex>
+#include <thread>
+
 #include "dabgpu.h"
+#include "fib_processor.h"
+#include "msc_consumers.h"
 
 namespace dabgpu {
 
 typedef std::complex<float> DSPCOMPLEX;   // dab-constants.h: DSPCOMPLEX
+
+// ---- reference data types (dab-constants.h:72-73,137-176) -------------------------
+#define DAB      0100
+#define DAB_PLUS 0101
+struct DabParams {
+    uint8_t dabMode;
+    int16_t L, K, T_null;
+    int32_t T_F;
+    int16_t T_s, T_u, guardLength, carrierDiff;
+};
+// RadioInterface::setModeParameters (gui.cpp:1361-1371); the GPU path is Mode I only
+void setModeParameters(DabParams *p, uint8_t mode = 1);
+// packetdata / audiodata (dab-constants.h:152-177): fib_processor.h
+
+// virtualInput (src/input/virtual-input.h:51-70): the device the front end pulls
+// samples from; getSamples copies up to n cf32 samples scaled to about +-1.
+class virtualInput {
+public:
+    virtual ~virtualInput() = default;
+    virtual int32_t getSamples(DSPCOMPLEX *v, int32_t n) = 0;
+    virtual int32_t Samples() = 0;
+    virtual bool restartReader() { return true; }
+    virtual void stopReader() {}
+    virtual int16_t bitDepth() { return 10; }
+};
 
 struct error : std::runtime_error {
     int code;
@@ -124,6 +157,172 @@ private:
     int index_ = 0, ficno_ = 0;
     int good_ = 0, total_ = 0;
     devbuf in_, bits_, crc_;
+};
+
+// ---- MSC back end ----------------------------------------------------------------
+// mp4Processor::addtoFrame / processSuperframe (mp4processor.cpp:107-292) minus faad:
+// 5-CIF superframe window, fire code, RS(120,110) of the RSDims columns on the GPU
+// (one dabgpu_rs_decode launch per superframe), AU table and AU CRCs; each AU goes to
+// the callback where the reference hands it to the AAC decoder.
+class mp4Processor : public dabProcessor {
+public:
+    struct au_info {
+        uint8_t dacRate, sbrFlag, aacChannelMode, mpegSurround;
+        int16_t n_corrected;           // RS symbols corrected in the superframe
+    };
+    using au_cb = std::function<void(const uint8_t *au, int16_t len, bool crc_ok, const au_info &)>;
+    mp4Processor(int16_t bitRate, au_cb cb);
+    void addtoFrame(uint8_t *v, int16_t nbits) override;
+    int32_t superframes() const { return superframes_; }
+    int32_t frameErrors() const { return frameErrors_; }
+private:
+    bool processSuperframe(int base);
+    int16_t bitRate_, RSDims_;
+    au_cb cb_;
+    std::vector<uint8_t> frameBytes_, outVector_;
+    int16_t blockFillIndex_ = 0, blocksInBuffer_ = 0;
+    int32_t superframes_ = 0, frameErrors_ = 0;
+    devbuf rsin_, rsout_, rsret_;
+};
+
+// dabConcurrent (dab-concurrent.cpp:34-202) without its thread: each CIF fragment is
+// time-de-interleaved (16 branches, delays 15 - brev4(i), the first 16 CIFs are warm-up),
+// then depunctured + Viterbi-decoded + energy-dispersed on the GPU
+// (dabgpu_msc_deconvolve) and handed to the dabProcessor.  (The reference's thread hands
+// CIF n over when CIF n+1 arrives; here it is decoded on arrival.)
+class dabConcurrent : public dabVirtual {
+public:
+    dabConcurrent(uint8_t dabModus, int16_t fragmentSize, int16_t bitRate, int16_t uepFlag, int16_t protLevel,
+                  std::unique_ptr<dabProcessor> processor);
+    int32_t process(int16_t *v, int16_t cnt) override;
+    dabProcessor *processor() { return proc_.get(); }
+protected:
+    bool deinterleave(const int16_t *v);       // false during the warm-up
+    int16_t fragmentSize_, bitRate_;
+    dabgpu_subch sub_;
+    std::vector<int16_t> delay_;               // [16][fragmentSize] ring of past fragments
+    std::vector<int16_t> data_;
+    int32_t countforInterleaver_ = 0, cif_ = 0;
+    std::vector<uint8_t> outV_;
+    std::unique_ptr<dabProcessor> proc_;
+    devbuf in_, out_;
+};
+
+// mscDatagroup (msc-datagroup.cpp:44-339) without its thread: the same de-interleave and
+// GPU decode, then packets -> MSC data groups (packetAssembler) for the data handler.
+class mscDatagroup : public dabConcurrent {
+public:
+    mscDatagroup(uint8_t DSCTy, int16_t packetAddress, int16_t fragmentSize, int16_t bitRate, int16_t uepFlag,
+                 int16_t protLevel, uint8_t DGflag, int16_t FEC_scheme, packetAssembler::datagroup_cb cb);
+    int32_t process(int16_t *v, int16_t cnt) override;
+    const packetAssembler &assembler() const { return pa_; }
+private:
+    packetAssembler pa_;
+};
+
+// mscHandler (msc-handler.cpp:41-193): collects the 18 MSC symbols of a CIF
+// (process_mscBlock with blkno 4..75), and for the selected subchannel hands the
+// CIF's slice [startAddr * 64, + Length * 64) to a dabConcurrent (audio: mp2Processor
+// for DAB, mp4Processor for DAB+ (ASCTy 077)) or an mscDatagroup (data).  The channel
+// set by set_audioChannel / set_dataChannel (any thread, under the lock) takes effect
+// at the next process_mscBlock.  The decoded output goes to the callbacks.
+class mscHandler {
+public:
+    struct outputs {
+        mp2Processor::frame_cb mp2;            // MPEG-1/2 layer II frames (DAB)
+        mp4Processor::au_cb aac;               // AAC access units (DAB+)
+        packetAssembler::datagroup_cb datagroup;
+    };
+    mscHandler(DabParams *p, outputs out, uint8_t concurrent = 1);
+    void process_mscBlock(int16_t *fbits, int16_t blkno);
+    void set_audioChannel(audiodata *d);
+    void set_dataChannel(packetdata *d);
+    int16_t getLanguage();
+    int16_t getType();
+    void stop();
+    void stopProcessing();
+    dabVirtual *handler() { return dabHandler_.get(); }
+private:
+    std::mutex locker_;
+    outputs out_;
+    int16_t BitsperBlock_, numberofblocksperCIF_;
+    std::vector<int16_t> cifVector_;
+    std::unique_ptr<dabVirtual> dabHandler_;
+    bool audioService_ = true, work_to_be_done_ = false, newChannel_ = false;
+    int16_t startAddr_ = 0, Length_ = 0;
+    audiodata na_{};
+    packetdata np_{};
+    int16_t new_language_ = 0, new_type_ = 0;
+};
+
+// ---- OFDM front end ----------------------------------------------------------------
+// ofdmDecoder (ofdm-decoder.cpp:85-230) one symbol per call on the GPU: processBlock_0
+// = get_snr (IIR 0.7/0.3, show_snr every 11 blocks) + coarse offset of freqSyncMethod
+// 0/1/2 + the spectrum as phase reference; processToken = FFT + DQPSK + frequency
+// de-interleave -> 3072 soft bits.  Samples are the caller's, already NCO-mixed.
+class ofdmDecoder {
+public:
+    ofdmDecoder(DabParams *p, uint8_t freqSyncMethod = 1, std::function<void(int)> show_snr = nullptr);
+    int16_t processBlock_0(DSPCOMPLEX *vi, bool flag);
+    void processToken(DSPCOMPLEX *inv, int16_t *ibits, int32_t blkno);
+    int16_t snr() const { return snr_; }
+private:
+    uint8_t method_;
+    std::function<void(int)> show_snr_;
+    int16_t snr_ = 0, snrCount_ = 0;
+    devbuf smp_, spec_, fr_, corr_, snrd_, bits_;
+};
+
+// ofdmProcessor (ofdm-processor.cpp:34-509): the constructor starts the thread that pulls
+// samples from the virtualInput into a sliding window in HBM and runs the GPU front end
+// (the dabgpu_pipe_* engine for one stream: null search, findIndex, coarse/fine AFC,
+// demod); every decoded frame's symbols go to ficHandler::process_ficBlock (blkno
+// 1..3) and mscHandler::process_mscBlock (4..75) with the reference's soft bits.  The
+// GUI signals are callbacks: show_fineCorrector / show_coarseCorrector (every
+// INPUT_RATE/7 samples, at frame granularity), show_avgTokenLength (every 11 frames),
+// setSynced, No_Signal_Found (scan mode) and show_snr.  startDumping writes the raw
+// samples as interleaved PCM16 (the .sdr payload) with the reference's scaling.
+class ficHandler;
+class ofdmProcessor {
+public:
+    struct signals {
+        std::function<void(int)> show_fineCorrector, show_coarseCorrector, show_avgTokenLength, show_snr;
+        std::function<void(char)> setSynced;
+        std::function<void()> No_Signal_Found;
+    };
+    ofdmProcessor(virtualInput *theRig, DabParams *p, signals sig, mscHandler *msc, ficHandler *fic,
+                  int16_t threshold = 3, uint8_t freqSyncMethod = 1);
+    ~ofdmProcessor();
+    void reset();
+    void stop();
+    void coarseCorrectorOn();
+    void coarseCorrectorOff();
+    void set_scanMode(bool b);
+    void startDumping(FILE *f);
+    void stopDumping();
+    int64_t frames() const { return frames_.load(); }
+private:
+    void run();
+    void emit_frame(const dabgpu_frame_info &fi);
+    virtualInput *theRig_;
+    signals sig_;
+    mscHandler *msc_;
+    ficHandler *fic_;
+    int16_t threshold_;
+    uint8_t method_;
+    std::thread thread_;
+    std::atomic<bool> running_{false};
+    std::atomic<int64_t> frames_{0};
+    std::mutex ctl_;
+    std::vector<int> pending_ops_;
+    std::atomic<FILE *> dumpFile_{nullptr};
+    int16_t dumpScaler_ = 512;
+    // observables state
+    int64_t sampleCnt_ = 0, last_block0_ = -1, prev_window_ = -1;
+    int32_t avgTokenLength_ = 196608, tokenCount_ = 0;
+    int16_t snr_ = 0, snrCount_ = 0;
+    int32_t no_signal_ = 0, resyncs_ = 0;
+    bool synced_ = false;
 };
 
 // The streaming engine: ofdmProcessor::run + ficHandler + mscHandler (+ DAB+

@@ -1,8 +1,12 @@
 // TEST INFRASTRUCTURE: the C++ drop-in classes (sdr-j-dab_amd/host) on the GPU
 // against the CPU oracle (oracle/liboracle.so) and the synthetic transmitter.
 // Prints one line per check and "DROPIN OK" at the end; exit code 0 on success.
+#include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <mutex>
+#include <thread>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -263,6 +267,181 @@ int main() {
             CHECK(sf_ok >= 1, "self-configured DAB+ superframes %d", sf_ok);
             std::printf("fib_processor + ensembleDecoder: ok (%d MSC CIF-subchannels, %d superframes)\n", msc_n, sf_ok);
         }
+    }
+    // ---- the reference-boundary classes: ofdmDecoder, ofdmProcessor (+ virtualInput),
+    // ficHandler, mscHandler (+ dabConcurrent, mp4Processor) against the oracle's
+    // sequential restatement of the same reference path on the same IQ
+    {
+        dabsynth_subch sc[2] = {{0, 96, 128, 3, 1, 0}, {96, 48, 64, 0103, 0, 1}};
+        dabsynth_cfg cfg;
+        std::memset(&cfg, 0, sizeof cfg);
+        const int NF = 24;
+        cfg.n_frames = NF + 1;
+        cfg.pre_offset = 50000;
+        cfg.snr_db = 22.0f;
+        cfg.cfo_hz = 300.0f;
+        cfg.amplitude = 1.0f;
+        cfg.n_subch = 2;
+        cfg.subch = sc;
+        const int64_t n = dabsynth_stream_len(&cfg);
+        std::vector<float> iq(2 * n);
+        int64_t f0 = 0;
+        CHECK(dabsynth_generate(&cfg, 4242, iq.data(), nullptr, nullptr, nullptr, &f0) == 0, "synth");
+        std::vector<orc_frame_info> info(NF + 1);
+        std::vector<int16_t> soft((size_t)(NF + 1) * 75 * 3072);
+        // the oracle stops where the reference would wait for more samples; the stream's
+        // last frame may or may not be complete to it -- the drop-in must decode at least
+        // as many frames, and the same FIBs / AUs for those
+        const int nf = orc_ofdm_run(iq.data(), n, 3, 1, NF + 1, info.data(), soft.data());
+        CHECK(nf >= NF, "oracle frames %d", nf);
+        // oracle: FIBs, and the DAB+ subchannel through dabConcurrent + mp4Processor
+        std::vector<std::vector<uint8_t>> ofib;
+        std::vector<int> ofib_ok;
+        for (int f = 0; f < nf; f++)
+            for (int b = 0; b < 4; b++) {
+                std::vector<uint8_t> bits(768), ok(3);
+                orc_fic_process(soft.data() + (size_t)f * 75 * 3072 + 2304 * b, bits.data(), ok.data());
+                for (int q = 0; q < 3; q++) {
+                    ofib.emplace_back(bits.begin() + 256 * q, bits.begin() + 256 * (q + 1));
+                    ofib_ok.push_back(ok[q]);
+                }
+            }
+        const int NC = 4 * nf, frag = 48 * 64;
+        std::vector<int16_t> cf((size_t)NC * frag);
+        for (int c = 0; c < NC; c++)
+            std::memcpy(&cf[(size_t)c * frag], soft.data() + ((size_t)(c / 4) * 75 + 3 + 18 * (c % 4)) * 3072 + 96 * 64,
+                        sizeof(int16_t) * frag);
+        std::vector<uint8_t> omsc((size_t)NC * 24 * 64);
+        CHECK(orc_msc_stream(0, 64, 0103, frag, NC, cf.data(), omsc.data()) == 0, "oracle msc");
+        std::vector<std::pair<std::vector<uint8_t>, bool>> oau;
+        orc_mp4 m4;
+        orc_mp4_init(&m4, 64);
+        for (int c = 16; c < NC; c++) {
+            uint8_t out[110 * 48];
+            int16_t nc, aus[8];
+            int na;
+            uint8_t crc[8];
+            if (orc_mp4_add(&m4, omsc.data() + (size_t)c * 24 * 64, out, &nc, &na, aus, crc) == 3)
+                for (int a = 0; a < na; a++)
+                    oau.push_back({std::vector<uint8_t>(out + aus[a], out + aus[a + 1] - 2), crc[a] != 0});
+        }
+        // ofdmDecoder one symbol at a time on frame 1 (its samples mixed by the oracle's NCO:
+        // the transmitter's CFO makes the NCO phase nonzero, so the test mixes them too)
+        {
+            dabgpu::DabParams p;
+            dabgpu::setModeParameters(&p, 1);
+            dabgpu::ofdmDecoder od(&p, 1);
+            const orc_frame_info &fi = info[1];
+            const int64_t b0 = fi.window_start + fi.start_index;
+            auto mixed = [&](int64_t first, int64_t count, int32_t lp0, int32_t phase, int64_t origin) {
+                std::vector<float> v(2 * count);
+                for (int64_t i = 0; i < count; i++) {
+                    const int64_t k = first + i - origin + 1;
+                    int64_t t = ((int64_t)lp0 - k * phase) % 2048000;
+                    if (t < 0) t += 2048000;
+                    float ore, oim;
+                    orc_osc_entry((int32_t)t, &ore, &oim);
+                    const float x = iq[2 * (first + i)], y = iq[2 * (first + i) + 1];
+                    volatile float ac = x * ore, bd = y * oim, ad = x * oim, bc = y * ore;
+                    v[2 * i] = ac - bd;
+                    v[2 * i + 1] = ad + bc;
+                }
+                return v;
+            };
+            const int32_t pa = fi.coarse + fi.fine;   // frame 1: no coarse correction in between
+            auto blk0 = mixed(b0, 2048, fi.lp_window, pa, fi.window_start);
+            float pref[4096];
+            const int16_t oc = orc_process_block0(blk0.data(), pref, 1, 1);
+            const int16_t gc = od.processBlock_0((dabgpu::DSPCOMPLEX *)blk0.data(), true);
+            CHECK(oc == gc, "ofdmDecoder::processBlock_0 %d vs %d", gc, oc);
+            int64_t lp_d = ((int64_t)fi.lp_window - (int64_t)(2048 + fi.start_index) * pa) % 2048000;
+            if (lp_d < 0) lp_d += 2048000;
+            long bad = 0, big = 0;
+            for (int l = 1; l < 76; l++) {
+                auto sym = mixed(b0 + 2048 + (int64_t)(l - 1) * 2552, 2552, (int32_t)lp_d, pa, b0 + 2048);
+                int16_t gi[3072], oi[3072];
+                od.processToken((dabgpu::DSPCOMPLEX *)sym.data(), gi, l);
+                orc_process_token(sym.data(), pref, oi, nullptr);
+                for (int i = 0; i < 3072; i++) {
+                    bad += gi[i] != oi[i];
+                    big += std::abs(gi[i] - oi[i]) > 1;
+                }
+            }
+            CHECK(big == 0 && bad <= 30, "ofdmDecoder::processToken: %ld soft bits differ (%ld by more than 1)", bad, big);
+            std::printf("ofdmDecoder: ok (%ld of %d soft bits at a rounding boundary)\n", bad, 75 * 3072);
+        }
+        // ofdmProcessor pulling from a virtualInput, feeding ficHandler and mscHandler
+        struct MemInput : dabgpu::virtualInput {
+            const float *iq;
+            int64_t n, pos = 0;
+            std::mutex m;
+            int32_t getSamples(dabgpu::DSPCOMPLEX *v, int32_t k) override {
+                std::lock_guard<std::mutex> g(m);
+                k = (int32_t)std::min<int64_t>(k, n - pos);
+                std::memcpy((void *)v, iq + 2 * pos, sizeof(float) * 2 * k);
+                pos += k;
+                return k;
+            }
+            int32_t Samples() override {
+                std::lock_guard<std::mutex> g(m);
+                return (int32_t)std::min<int64_t>(40000, n - pos);   // arrives in pieces, like a device
+            }
+        } input;
+        input.iq = iq.data();
+        input.n = n;
+        std::mutex mu;
+        std::vector<std::vector<uint8_t>> gfib;
+        std::vector<int> gfib_ok;
+        std::vector<std::pair<std::vector<uint8_t>, bool>> gau;
+        int synced_true = 0, snr_shown = 0, tok_shown = 0, fine_shown = 0, last_tok = 0;
+        dabgpu::ficHandler fh([&](const uint8_t *fib, bool ok, int16_t) {
+            std::lock_guard<std::mutex> g(mu);
+            gfib.emplace_back(fib, fib + 256);
+            gfib_ok.push_back(ok);
+        });
+        dabgpu::DabParams p;
+        dabgpu::setModeParameters(&p, 1);
+        dabgpu::mscHandler::outputs outs;
+        outs.aac = [&](const uint8_t *au, int16_t len, bool ok, const dabgpu::mp4Processor::au_info &) {
+            std::lock_guard<std::mutex> g(mu);
+            gau.push_back({std::vector<uint8_t>(au, au + len), ok});
+        };
+        dabgpu::mscHandler mh(&p, outs, 1);
+        dabgpu::audiodata ad{1, 96, 1, 0103, 48, 64, 077, 0, 0};
+        mh.set_audioChannel(&ad);
+        dabgpu::ofdmProcessor::signals sig;
+        sig.setSynced = [&](char b) { synced_true += b ? 1 : 0; };
+        sig.show_snr = [&](int) { snr_shown++; };
+        sig.show_avgTokenLength = [&](int v) { tok_shown++; last_tok = v; };
+        sig.show_fineCorrector = [&](int) { fine_shown++; };
+        {
+            dabgpu::ofdmProcessor op(&input, &p, sig, &mh, &fh, 3, 1);
+            auto t0 = std::chrono::steady_clock::now();
+            while (op.frames() < NF + 1 && std::chrono::steady_clock::now() - t0 < std::chrono::seconds(60))
+                std::this_thread::sleep_for(std::chrono::milliseconds(20));
+            std::this_thread::sleep_for(std::chrono::milliseconds(200));
+            CHECK(op.frames() >= nf && op.frames() <= NF + 1, "ofdmProcessor decoded %lld frames, the reference %d",
+                  (long long)op.frames(), nf);
+        }
+        std::lock_guard<std::mutex> g(mu);
+        int fib_diff = 0;
+        for (size_t i = 0; i < std::min(gfib.size(), ofib.size()); i++)
+            fib_diff += gfib[i] != ofib[i] || gfib_ok[i] != ofib_ok[i];
+        CHECK(gfib.size() >= ofib.size() && gfib.size() <= (size_t)(NF + 1) * 12 && fib_diff == 0,
+              "ofdmProcessor+ficHandler: %zu FIBs vs %zu, %d differ",
+              gfib.size(), ofib.size(), fib_diff);
+        int au_diff = 0, au_ok = 0;
+        for (size_t i = 0; i < std::min(gau.size(), oau.size()); i++) {
+            au_diff += gau[i] != oau[i];
+            au_ok += gau[i].second;
+        }
+        CHECK(gau.size() >= oau.size() && gau.size() <= oau.size() + 16 && au_diff == 0 && au_ok > 0, "mscHandler DAB+ AUs: %zu vs %zu, %d differ",
+              gau.size(), oau.size(), au_diff);
+        CHECK(synced_true >= 1 && snr_shown >= 2 && tok_shown >= 1 && fine_shown >= 1 &&
+                  std::abs(last_tok - 196608) < 20, "observables synced %d snr %d token %d (%d) fine %d", synced_true,
+              snr_shown, tok_shown, last_tok, fine_shown);
+        std::printf("ofdmProcessor + ficHandler + mscHandler: ok (%zu FIBs, %zu AUs, %d with good CRC)\n", gfib.size(),
+                    gau.size(), au_ok);
     }
     if (failures) {
         std::printf("DROPIN FAILED (%d)\n", failures);

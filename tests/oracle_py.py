@@ -179,3 +179,147 @@ def decode_streams(iqs, max_frames, subch, method=1, threads=16):
     oracle()
     with ThreadPoolExecutor(max_workers=max(1, threads)) as ex:
         return list(ex.map(lambda x: decode_stream(x, max_frames, subch, method), iqs))
+
+
+# ---- MSC consumers (host code in the product; restated here as the checker) --------
+def check_crc_bits(bits):
+    """check_CRC_bits (dab-constants.h:310-340) on a bit list; inverts the last 16 in place"""
+    n = len(bits)
+    for i in range(n - 16, n):
+        bits[i] ^= 1
+    b = [1] * 16
+    poly = [0, 0, 0, 1, 0, 0, 0, 0, 0, 0, 1, 0, 0, 0, 0]
+    for i in range(n):
+        if (b[0] ^ bits[i]) == 1:
+            for f in range(15):
+                b[f] = poly[f] ^ b[f + 1]
+            b[15] = 1
+        else:
+            b[:15] = b[1:16]
+            b[15] = 0
+    return sum(b) == 0
+
+
+class MP2:
+    """mp2Processor::addtoFrame (mp2processor.cpp:572-629): 12-one sync, 24-bit header
+    (sample rate via mp2sampleRate :276-285, setSamplerate :262-269), frame of 24*bitRate
+    bits (twice that at 24 kHz).  frames: list of (bytes, sampleRate)."""
+    RATES = [44100, 48000, 32000, 0, 22050, 24000, 16000, 0]
+
+    def __init__(self, bitrate):
+        self.size = 24 * bitrate
+        self.frame = bytearray(2 * self.size)
+        self.ok = self.hc = self.bc = 0
+        self.baud = 48000
+        self.frames = []
+
+    def _bit(self, b, nm):
+        if b:
+            self.frame[nm // 8] |= 1 << (7 - (nm & 7))
+        else:
+            self.frame[nm // 8] &= ~(1 << (7 - (nm & 7))) & 0xFF
+
+    def add(self, bits):
+        lf = self.size if self.baud == 48000 else 2 * self.size
+        for v in bits:
+            if self.ok == 2:
+                self._bit(v, self.bc)
+                self.bc += 1
+                if self.bc >= lf:
+                    self.frames.append((bytes(self.frame[:lf // 8]), self.baud))
+                    self.ok = self.hc = self.bc = 0
+            elif self.ok == 0:
+                if v == 1:
+                    self.hc += 1
+                    if self.hc == 12:
+                        self.bc = 0
+                        for _ in range(12):
+                            self._bit(1, self.bc)
+                            self.bc += 1
+                        self.ok = 1
+                else:
+                    self.hc = 0
+            else:
+                self._bit(v, self.bc)
+                self.bc += 1
+                if self.bc == 24:
+                    f = self.frame
+                    rate = 0
+                    if f[0] == 0xFF and (f[1] & 0xF6) == 0xF4 and f[2] - 0x10 < 0xE0:
+                        rate = MP2.RATES[(((f[1] & 0x08) >> 1) ^ 4) + ((f[2] >> 2) & 3)]
+                    if rate in (48000, 24000):
+                        self.baud = rate
+                    self.ok = 2
+            lf = self.size if self.baud == 48000 else 2 * self.size
+
+
+class Datagroups:
+    """mscDatagroup::handlePackets / handlePacket / handleTDCAsyncstream
+    (msc-datagroup.cpp:221-339): groups = list of data-group bit lists."""
+
+    def __init__(self, dscty, dgflag):
+        self.dscty, self.dgflag = dscty, dgflag
+        self.state, self.addr, self.series = 0, -1, []
+        self.groups, self.crc_errors = [], 0
+
+    @staticmethod
+    def _get(d, off, n):
+        r = 0
+        for i in range(n):
+            r = (r << 1) | d[off + i]
+        return r
+
+    def add(self, bits):
+        data = list(bits)
+        if self.dscty == 5 and self.dgflag:
+            pl = (self._get(data, 0, 2) + 1) * 24
+            seg = data[:pl * 8]
+            check_crc_bits(seg)
+            return
+        pos, length = 0, len(data)
+        while True:
+            plen = (self._get(data, pos, 2) + 1) * 24 * 8
+            if length < plen:
+                return
+            self._packet(data, pos)
+            length -= plen
+            if length < 2:
+                return
+            pos += plen
+
+    def _packet(self, data, pos):
+        g = lambda o, n: self._get(data, pos + o, n)
+        plen = (g(0, 2) + 1) * 24
+        fl, address, useful = g(4, 2), g(6, 10), g(17, 7)
+        seg = data[pos:pos + plen * 8]
+        ok = check_crc_bits(seg)
+        data[pos:pos + plen * 8] = seg
+        if not ok:
+            self.crc_errors += 1
+            return
+        if address == 0:
+            return
+        if self.addr == -1:
+            self.addr = address
+        if self.addr != address:
+            return
+        take = data[pos + 24:pos + 24 + 8 * useful]
+        if self.state == 0:
+            if fl == 2:
+                self.state, self.series = 1, list(take)
+            elif fl == 3:
+                self.series = list(take)
+                self.groups.append(list(self.series))
+            else:
+                self.series = []
+        else:
+            if fl == 0:
+                self.series += take
+            elif fl == 1:
+                self.series += take
+                self.groups.append(list(self.series))
+                self.state = 0
+            elif fl == 2:
+                self.state, self.series = 1, list(take)
+            else:
+                self.state, self.series = 0, []
