@@ -104,10 +104,16 @@ typedef struct {
 /* ---- host-side tables (no device needed; for pinning against the reference) --
  *   DABGPU_TABLE_PRS     float2[2048] refTable (phasereference.cpp:40-47), natural order
  *   DABGPU_TABLE_MAPPER  int16[1536]  permVector::mapIn (mapper.cpp:33-117)
- *   DABGPU_TABLE_REFARG  float[18]    refArg (ofdm-decoder.cpp:71-74) */
+ *   DABGPU_TABLE_REFARG  float[18]    refArg (ofdm-decoder.cpp:71-74)
+ *   DABGPU_TABLE_OSC     float2[2048000] oscillatorTable (ofdm-processor.cpp:79-81)
+ *   DABGPU_TABLE_NCO     double2[384] the factor tables the kernels rebuild
+ *                        oscillatorTable from (128 e^{2pi i a/128}, 125 e^{2pi i b/16000},
+ *                        128 e^{2pi i c/2048000}, 3 zero) */
 #define DABGPU_TABLE_PRS    1
 #define DABGPU_TABLE_MAPPER 2
 #define DABGPU_TABLE_REFARG 3
+#define DABGPU_TABLE_OSC    4
+#define DABGPU_TABLE_NCO    5
 int dabgpu_host_table(int which, void *out_h, size_t bytes);
 /* The depuncturing profile the decoder uses for a subchannel (deconvolve.cpp:142-366;
  * uep_deconvolve's unknown-profile fallback to table row 1, :148-151): decoded bits,
@@ -186,6 +192,10 @@ int dabgpu_ofdm_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *fr
 int dabgpu_ofdm_sync_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n, int16_t level,
                            int32_t *start_index_d, int16_t *snr_d, int16_t *softbits_d, float *softf_d,
                            float *freqcorr_d);
+
+/* The kernels' NCO: oscillatorTable[first .. first+n-1] as the front-end kernels
+ * compute it (float2 into out_d) -- for checking it against the table exhaustively. */
+int dabgpu_nco_eval(dabgpu_ctx *ctx, int32_t first, int32_t n, float *out_d);
 
 /* One symbol at a time (the reference's ofdmDecoder call pattern, ofdm-decoder.cpp:
  * 85-190), samples already mixed by the caller: kind 0 = block 0 (samples_d holds

@@ -14,8 +14,17 @@ constexpr int INPUT_RATE = 2048000;
 
 // device tables for the OFDM kernels (built on the host with the reference's
 // own float expressions, see dabgpu.cpp: make_tables)
+// The NCO without its 16 MB table: oscillatorTable[t] (ofdm-processor.cpp:79-81) is
+// float(e^{2 pi i t / 2048000}); with t = 16000 a + 128 b + c it is the float rounding
+// of A[a] (B[b] C[c]) in double (fma complex products), A[a] = e^{2 pi i a/128},
+// B[b] = e^{2 pi i b/16000}, C[c] = e^{2 pi i c/2048000}: 381 double2 that fit in LDS.
+// The rounded product equals the table at every one of the 2048000 indices
+// (tests/cpp/test_nco.c on the host, test_gpu_parity's exhaustive check on the GPU).
+constexpr int NCO_A = 0, NCO_B = 128, NCO_C = 253, NCO_N = 384;
+
 struct OfdmTables {
     const float2 *osc;      // oscillatorTable[2048000] (ofdm-processor.cpp:79-81)
+    const double2 *nco;     // the factor tables above, [NCO_N]
     const float2 *ref;      // PRS refTable[2048] (phasereference.cpp:40-47), natural bin order
     const float *refarg;    // refArg[18] (ofdm-decoder.cpp:71-74)
     const float2 *w2048;    // W2048^j = e^{-2 pi i j/2048}, j < 2048 (double, rounded to float)
@@ -135,6 +144,7 @@ hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr
 hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
                         const DemodAux &aux);
+hipError_t launch_nco_eval(hipStream_t st, const OfdmTables &T, int32_t first, int32_t n, float2 *out);
 hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmTables &T, float *spec, int16_t *ibits);
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
 hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,

@@ -63,6 +63,7 @@ float get_phi(int k) {                                   // phasetable.cpp:261-2
 
 struct HostTables {
     std::vector<float2> osc;
+    std::vector<double2> nco;               // factor tables of the NCO (dab_kernels.h)
     std::vector<uint32_t> prbs_words;
     std::vector<float2> w2048;
     std::vector<int16_t> carrier_bin;
@@ -74,6 +75,11 @@ struct HostTables {
         osc.resize(M);
         for (int i = 0; i < M; i++)          // ofdm-processor.cpp:79-81
             osc[i] = make_float2((float)cos(2.0 * M_PI * i / M), (float)sin(2.0 * M_PI * i / M));
+        nco.assign(NCO_N, make_double2(0.0, 0.0));
+        for (int k = 0; k < 128; k++) nco[NCO_A + k] = make_double2(cos(2.0 * M_PI * k / 128), sin(2.0 * M_PI * k / 128));
+        for (int k = 0; k < 125; k++)
+            nco[NCO_B + k] = make_double2(cos(2.0 * M_PI * k / 16000), sin(2.0 * M_PI * k / 16000));
+        for (int k = 0; k < 128; k++) nco[NCO_C + k] = make_double2(cos(2.0 * M_PI * k / M), sin(2.0 * M_PI * k / M));
         ref.assign(2048, make_float2(0.0f, 0.0f));
         for (int i = 1; i <= 768; i++) {      // phasereference.cpp:42-47
             float phi = get_phi(i);
@@ -257,6 +263,7 @@ struct dabgpu_ctx {
     hipStream_t stream = nullptr;
     hipEvent_t ev[16] = {};
     float2 *osc = nullptr, *ref = nullptr;
+    double2 *nco = nullptr;
     uint32_t *prbs = nullptr;
     float2 *w2048 = nullptr;
     int16_t *carrier_bin = nullptr;
@@ -314,6 +321,8 @@ int dabgpu_host_table(int which, void *out, size_t bytes) {
     case DABGPU_TABLE_PRS: src = t.ref.data(); n = t.ref.size() * sizeof(float2); break;
     case DABGPU_TABLE_MAPPER: src = t.perm.data(); n = t.perm.size() * sizeof(int16_t); break;
     case DABGPU_TABLE_REFARG: src = t.refarg.data(); n = t.refarg.size() * sizeof(float); break;
+    case DABGPU_TABLE_NCO: src = t.nco.data(); n = t.nco.size() * sizeof(double2); break;
+    case DABGPU_TABLE_OSC: src = t.osc.data(); n = t.osc.size() * sizeof(float2); break;
     default: return fail(DABGPU_E_ARG, "unknown table %d", which);
     }
     if (!out || bytes < n) return fail(DABGPU_E_ARG, "table %d needs %zu bytes", which, n);
@@ -371,7 +380,7 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     const HostTables &t = host_tables();
     int rc = 0;
-    if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->ref, t.ref)) ||
+    if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->nco, t.nco)) || (rc = upload(c, &c->ref, t.ref)) ||
         (rc = upload(c, &c->w2048, t.w2048)) || (rc = upload(c, &c->carrier_bin, t.carrier_bin)) ||
         (rc = upload(c, &c->prbs, t.prbs_words)) ||
         (rc = upload(c, &c->refarg, t.refarg)) || (rc = upload(c, &c->dptab, t.dptab))) {
@@ -379,6 +388,7 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
         return rc;
     }
     c->T.osc = c->osc;
+    c->T.nco = c->nco;
     c->T.ref = c->ref;
     c->T.w2048 = c->w2048;
     c->T.carrier_of_bin = c->carrier_bin;
@@ -397,7 +407,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     if (!c) return 0;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
-    for (void *p : {(void *)c->osc, (void *)c->ref, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
+    for (void *p : {(void *)c->osc, (void *)c->nco, (void *)c->ref, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
                     (void *)c->refarg, (void *)c->err, (void *)c->dptab})
         if (p) (void)hipFree(p);
     if (c->h_err) (void)hipHostFree(c->h_err);
@@ -533,6 +543,11 @@ int dabgpu_ofdm_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, in
 int dabgpu_ofdm_symbol(dabgpu_ctx *c, const float *smp, int kind, float *spec, int16_t *ibits) {
     if (!c || !smp || !spec || (kind != 0 && kind != 1) || (kind == 1 && !ibits)) return fail(DABGPU_E_ARG, "bad args");
     HIPCHK(launch_symbol(c->stream, smp, kind, c->T, spec, ibits));
+    return 0;
+}
+int dabgpu_nco_eval(dabgpu_ctx *c, int32_t first, int32_t n, float *out) {
+    if (!c || !out || first < 0 || n < 0 || (int64_t)first + n > M) return fail(DABGPU_E_ARG, "bad args");
+    if (n) HIPCHK(launch_nco_eval(c->stream, c->T, first, n, (float2 *)out));
     return 0;
 }
 int dabgpu_ofdm_sync_demod(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t level, int32_t *si,

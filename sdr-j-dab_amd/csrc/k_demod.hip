@@ -86,9 +86,13 @@ __device__ __forceinline__ float quad_bfly(float v, float sign) {
     return fmaf(sign, v, p);
 }
 
+// v[m] *= oscillatorTable[localPhase] sample by sample (ofdm-processor.cpp:186-201).
+// GEN: localPhase steps by -phase per sample, the table rebuilt from the factor tables
+// in LDS (nco_value; the 16 MB table itself would cost a cache line per sample);
+// otherwise phase == 0 and every sample uses oscillatorTable[lp0].
 template <bool GEN>
-__device__ __forceinline__ void mix(float2 (&v)[8], const float2 *__restrict__ osc, int32_t lp0, int32_t phase,
-                                   int64_t first, int64_t origin) {
+__device__ __forceinline__ void mix(float2 (&v)[8], const float2 *__restrict__ osc, const double2 *ncl, int32_t lp0,
+                                   int32_t phase, int64_t first, int64_t origin) {
     // v[m] = sample first + 256 m of a getSamples segment that started at `origin`
     if (!GEN || phase == 0) {
         const float2 f = osc[lp0];
@@ -99,17 +103,23 @@ __device__ __forceinline__ void mix(float2 (&v)[8], const float2 *__restrict__ o
         const int32_t step = (int32_t)((((int64_t)256 * phase) % INPUT_RATE + INPUT_RATE) % INPUT_RATE);
 #pragma unroll
         for (int m = 0; m < 8; m++) {
-            v[m] = cmul_exact(v[m], osc[t]);
+            v[m] = cmul_exact(v[m], nco_value(ncl, t));
             t -= step;
             if (t < 0) t += INPUT_RATE;
         }
     }
 }
 template <bool GEN>
-__device__ __forceinline__ float2 mix1(float2 v, const float2 *__restrict__ osc, int32_t lp0, int32_t phase,
-                                       int64_t pos, int64_t origin) {
+__device__ __forceinline__ float2 mix1(float2 v, const float2 *__restrict__ osc, const double2 *ncl, int32_t lp0,
+                                       int32_t phase, int64_t pos, int64_t origin) {
     if (!GEN || phase == 0) return cmul_exact(v, osc[lp0]);
-    return cmul_exact(v, osc[nco_index2(lp0, phase, pos - origin + 1)]);
+    return cmul_exact(v, nco_value(ncl, nco_index2(lp0, phase, pos - origin + 1)));
+}
+// the factor tables into LDS (GEN kernels only; callers __syncthreads before use)
+template <bool GEN>
+__device__ __forceinline__ void nco_setup(double2 *ncl, const OfdmTables &T, int t) {
+    if constexpr (GEN)
+        for (int i = t; i < NCO_N; i += DT) ncl[i] = T.nco[i];
 }
 
 struct DemodTw {
@@ -320,7 +330,9 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x;
+    __shared__ double2 ncl[GEN ? NCO_N : 1];
     const DemodTw tw = tw_setup(twl, T, t);
+    nco_setup<GEN>(ncl, T, t);
     __syncthreads();
     const int item = blockIdx.x;
     const int fi = item / nchunks, ch = item % nchunks;
@@ -342,7 +354,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             float2 a[8];
 #pragma unroll
             for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
-            mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
+            mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
             float mx, sm;
 #ifdef DEMOD_FAKE_SYNC  // A/B measurement only (tools/build_variant.sh): the frame's own block0
             const int32_t si = (int32_t)(fr.block0 - fr.window) + (a[0].x == 12345.0f ? 1 : 0);
@@ -390,8 +402,8 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
 #pragma unroll
             for (int m = 0; m < 8; m++) a[m] = s[u + t + 256 * m];
-            if (l0 == 1) mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, u + t, fr.window);
-            else mix<GEN>(a, T.osc, fr.lp_data, fr.phase_b, u + t, dorg);
+            if (l0 == 1) mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
+            else mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
         }
         {
             const int64_t u = fr.block0 + (int64_t)l0 * TS;
@@ -421,9 +433,9 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
 #pragma unroll
                 for (int m = 0; m < 8; m++) nx[m] = s[u1 + t + 256 * m];
             }
-            mix<GEN>(a, T.osc, fr.lp_data, fr.phase_b, u0 + t, dorg);
-            g6 = mix1<GEN>(g6, T.osc, fr.lp_data, fr.phase_b, u0 - 512 + t, dorg);
-            g7 = mix1<GEN>(g7, T.osc, fr.lp_data, fr.phase_b, u0 - 256 + t, dorg);
+            mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u0 + t, dorg);
+            g6 = mix1<GEN>(g6, T.osc, ncl, fr.lp_data, fr.phase_b, u0 - 512 + t, dorg);
+            g7 = mix1<GEN>(g7, T.osc, ncl, fr.lp_data, fr.phase_b, u0 - 256 + t, dorg);
             if (t >= 8) {                              // FreqCorr over i in [T_u, T_s)
                 const float2 p = cmul_conj_exact(a[6], g6);
                 fc.x += p.x; fc.y += p.y;
@@ -480,7 +492,9 @@ __global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, co
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x, f = blockIdx.x;
+    __shared__ double2 ncl[GEN ? NCO_N : 1];
     const DemodTw tw = tw_setup(twl, T, t);
+    nco_setup<GEN>(ncl, T, t);
     __syncthreads();
     const dabgpu_frame fr = frames[f];
     if (fr.window < 0 || fr.window + TU > fr.n_samples || fr.lp_window < 0 || fr.lp_window >= INPUT_RATE) {
@@ -494,7 +508,7 @@ __global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, co
     float2 a[8];
 #pragma unroll
     for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
-    mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
+    mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
     float mx, sm;
     const int32_t si = prs_corr_wg(a, ex, tw, t, T.ref, aux.level, red, mx, sm);
     if (t == 0) {
@@ -519,7 +533,9 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
     __shared__ float val[2048];                          // |X| (method 0) or per-candidate sums
     __shared__ float cv[96];                             // method 1: correlationVector
     const int t = threadIdx.x, f = blockIdx.x;
+    __shared__ double2 ncl[GEN ? NCO_N : 1];
     const DemodTw tw = tw_setup(twl, T, t);
+    nco_setup<GEN>(ncl, T, t);
     __syncthreads();
     const dabgpu_frame fr = frames[f];
     if (fr.window < 0 || fr.block0 < fr.window || fr.block0 + TU > fr.n_samples || fr.lp_window < 0 ||
@@ -535,7 +551,7 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
     float2 a[8];
 #pragma unroll
     for (int m = 0; m < 8; m++) a[m] = s[fr.block0 + t + 256 * m];
-    mix<GEN>(a, T.osc, fr.lp_window, fr.phase_a, fr.block0 + t, fr.window);
+    mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.block0 + t, fr.window);
     fft2048_wg(a, ex, tw, t);
     {
         const int16_t v = snr_wg(a, t, red);
@@ -646,6 +662,19 @@ __global__ __launch_bounds__(DT) void k_symbol_wg(const float2 *__restrict__ smp
         }
         spec[b] = a[k];
     }
+}
+
+// the kernels' NCO over a range of table indices (exhaustive parity check)
+__global__ __launch_bounds__(DT) void k_nco_eval(OfdmTables T, int32_t first, int32_t n, float2 *__restrict__ out) {
+    __shared__ double2 ncl[NCO_N];
+    nco_setup<true>(ncl, T, threadIdx.x);
+    __syncthreads();
+    for (int32_t i = blockIdx.x * DT + threadIdx.x; i < n; i += gridDim.x * DT) out[i] = nco_value(ncl, first + i);
+}
+hipError_t launch_nco_eval(hipStream_t st, const OfdmTables &T, int32_t first, int32_t n, float2 *out) {
+    const int blocks = (int)std::min<int64_t>(2048, ((int64_t)n + DT - 1) / DT);
+    hipLaunchKernelGGL(k_nco_eval, dim3(blocks), dim3(DT), 0, st, T, first, n, out);
+    return hipGetLastError();
 }
 
 hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmTables &T, float *spec, int16_t *ibits) {

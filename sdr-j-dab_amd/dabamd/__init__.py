@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
             "dabgpu_memset_d": ([vp, vp, i32, sz], i32),
             "dabgpu_memcpy_d2d": ([vp, vp, vp, sz], i32),
             "dabgpu_ofdm_symbol": ([vp, vp, i32, vp, vp], i32),
+            "dabgpu_nco_eval": ([vp, i32, i32, vp], i32),
             "dabgpu_iq_convert": ([vp, i32, vp, i64, vp], i32),
             "dabgpu_event_record": ([vp, i32], i32),
             "dabgpu_kernel_errors": ([vp], i32),
@@ -140,13 +141,14 @@ def _p(a: np.ndarray) -> C.c_void_p:
 
 
 IQ_U8, IQ_S16 = 1, 2   # dabgpu_iq_convert formats
-TABLE_PRS, TABLE_MAPPER, TABLE_REFARG = 1, 2, 3
+TABLE_PRS, TABLE_MAPPER, TABLE_REFARG, TABLE_OSC, TABLE_NCO = 1, 2, 3, 4, 5
 
 
 def host_table(which: int) -> np.ndarray:
     """the product's host-built tables (dabgpu_host_table; no device needed)"""
     shape, dt = {TABLE_PRS: ((2048, 2), np.float32), TABLE_MAPPER: (1536, np.int16),
-                 TABLE_REFARG: (18, np.float32)}[which]
+                 TABLE_REFARG: (18, np.float32), TABLE_OSC: ((2048000, 2), np.float32),
+                 TABLE_NCO: ((384, 2), np.float64)}[which]
     out = np.zeros(shape, dt)
     _chk(lib().dabgpu_host_table(which, _p(out), out.nbytes), "dabgpu_host_table")
     return out
@@ -426,6 +428,18 @@ class Context:
                 if b is not None:
                     b.free()
 
+
+    def nco_eval(self, first: int = 0, n: int = 2048000) -> np.ndarray:
+        """oscillatorTable[first:first+n] as the front-end kernels compute it
+        (dabgpu_nco_eval): float32 [n, 2]"""
+        d = self.buf(8 * n)
+        try:
+            _chk(lib().dabgpu_nco_eval(self.h, first, n, d.ptr), "nco_eval")
+            out = d.download(np.float32, (n, 2))
+            self.check()
+            return out
+        finally:
+            d.free()
 
     def sync_demod(self, iq: DevBuf, frames: Sequence[Frame], level: int = 3, with_float: bool = False):
         """findIndex + get_snr + processToken x 75 in one launch (dabgpu_ofdm_sync_demod).

@@ -165,6 +165,18 @@ def test_msc_golden(ctx):
 
 
 # ---------------------------------------------------------------- front end
+def test_nco_exhaustive(ctx):
+    """the kernels' NCO (dabgpu_nco_eval: LDS factor tables, FP64 fma products) equals
+    oscillatorTable (ofdm-processor.cpp:79-81) at all 2048000 indices, and at the
+    product's host table, which tests/cpp/test_nco.c pins to the oracle's"""
+    import dabamd
+    got = ctx.nco_eval(0, 2048000)
+    want = dabamd.host_table(dabamd.TABLE_OSC)
+    bad = np.nonzero((got.view(np.uint32) != want.view(np.uint32)).any(axis=1))[0]
+    assert len(bad) == 0, (len(bad), bad[:8], got[bad[:4]], want[bad[:4]])
+    assert np.array_equal(ctx.nco_eval(2047990, 10), want[2047990:])
+
+
 def _frames_from_oracle(info, n_samples, iq_base=0):
     import dabamd
     frs = []

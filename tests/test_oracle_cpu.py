@@ -107,6 +107,18 @@ def test_product_tables_match_reference_fixtures():
     assert np.allclose(got, np.angle(z).astype(np.float32), atol=1e-6)
 
 
+def test_nco_factor_tables_rebuild_oscillator_table_exactly():
+    """the front-end kernels' NCO (three double factor tables, fma products, rounded to
+    float) equals oscillatorTable (ofdm-processor.cpp:79-81) at all 2048000 indices; the
+    product's own table too (tests/cpp/test_nco.c)"""
+    import subprocess
+    subprocess.run(["make", "-s", "-f", os.path.join(ROOT, "tests", "cpp", "Makefile"),
+                    os.path.join(ROOT, "tests", "cpp", "build", "test_nco")], check=True)
+    r = subprocess.run([os.path.join(ROOT, "tests", "cpp", "build", "test_nco")], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_rs_matches_reference_fixtures():
     g = _g("rs_kat.npz")
     for cw, dec, ret in zip(g["cw"], g["dec"], g["ret"]):

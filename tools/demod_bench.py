@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--frames", type=int, default=24)
     ap.add_argument("--reps", type=int, default=30)
     ap.add_argument("--cfo", type=float, default=0.0)
+    ap.add_argument("--phase", type=int, default=0, help="NCO phase step of every frame (!= 0: the per-sample NCO)")
     a = ap.parse_args()
     import dabamd
     from dabamd.synth import Ensemble
@@ -43,7 +44,8 @@ def main():
         for k in range(F):
             b0 = f0 + k * 196608 + 2656 + 504
             frames.append(dabamd.Frame(iq_base=e * stride, n_samples=stride, window=b0 - 504, block0=b0,
-                                       out_slot=len(frames), flags=0))
+                                       out_slot=len(frames), flags=0, lp_window=123457 if a.phase else 0,
+                                       lp_data=654321 if a.phase else 0, phase_a=a.phase, phase_b=a.phase))
     n = len(frames)
     fa = (dabamd.Frame * n)(*frames)
     dfr = dabamd.DevBuf(ctx, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
