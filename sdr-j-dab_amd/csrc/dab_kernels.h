@@ -20,7 +20,7 @@ constexpr int INPUT_RATE = 2048000;
 // B[b] = e^{2 pi i b/16000}, C[c] = e^{2 pi i c/2048000}: 381 double2 that fit in LDS.
 // The rounded product equals the table at every one of the 2048000 indices
 // (tests/cpp/test_nco.c on the host, test_gpu_parity's exhaustive check on the GPU).
-constexpr int NCO_A = 0, NCO_B = 128, NCO_C = 253, NCO_N = 384;
+constexpr int NCO_A = 0, NCO_B = 128, NCO_C = 253, NCO_N = 384, NCO_USED = 381;
 
 struct OfdmTables {
     const float2 *osc;      // oscillatorTable[2048000] (ofdm-processor.cpp:79-81)

@@ -29,13 +29,27 @@ namespace dab {
 constexpr int DT = 256;                 // threads per demod workgroup
 constexpr int ZROW = 36;                // pass-2 output rows of 32 (+4 pad: conflict-free pass-3 reads)
 #ifndef DEMOD_WG_PER_SIMD
-#define DEMOD_WG_PER_SIMD 3     // resident workgroups per CU (= waves per SIMD): <= 168 VGPRs
+#define DEMOD_WG_PER_SIMD 4     // resident workgroups per CU (= waves per SIMD): <= 128 VGPRs, <= 40 KB LDS
 #endif
 
 __device__ __forceinline__ int32_t nco_index2(int32_t lp0, int32_t phase, int64_t j) {
     int64_t t = ((int64_t)lp0 - j * (int64_t)phase) % INPUT_RATE;
     return (int32_t)(t < 0 ? t + INPUT_RATE : t);
 }
+__device__ __forceinline__ int32_t nco_mod(int64_t v) {
+    const int64_t t = v % INPUT_RATE;
+    return (int32_t)(t < 0 ? t + INPUT_RATE : t);
+}
+// x - d, x + d mod INPUT_RATE for x, d in [0, INPUT_RATE)
+__device__ __forceinline__ int32_t nco_sub(int32_t x, int32_t d) {
+    x -= d;
+    return x < 0 ? x + INPUT_RATE : x;
+}
+__device__ __forceinline__ int32_t nco_add(int32_t x, int32_t d) {
+    x += d;
+    return x >= INPUT_RATE ? x - INPUT_RATE : x;
+}
+typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
 
 // (int16_t)(q * 127.0) exactly as the reference computes it: q promoted to double
 // (ofdm-decoder.cpp:188-189): 3 instructions (cvt, mul_f64, truncating cvt)
@@ -79,6 +93,7 @@ __device__ __forceinline__ void dft8(float2 (&a)[8]) {
 
 // radix-2 butterfly across lanes at xor distance M inside a quad:
 // lanes with bit M clear get v + partner, lanes with it set get partner - v
+// (a DPP move + fma; a v_mul + v_add_f32_dpp form measured 2 % slower in this kernel)
 template <int M>
 __device__ __forceinline__ float quad_bfly(float v, float sign) {
     constexpr int ctrl = M == 2 ? 0x4E : 0xB1;          // quad_perm [2,3,0,1] / [1,0,3,2]
@@ -119,7 +134,7 @@ __device__ __forceinline__ float2 mix1(float2 v, const float2 *__restrict__ osc,
 template <bool GEN>
 __device__ __forceinline__ void nco_setup(double2 *ncl, const OfdmTables &T, int t) {
     if constexpr (GEN)
-        for (int i = t; i < NCO_N; i += DT) ncl[i] = T.nco[i];
+        for (int i = t; i < NCO_USED; i += DT) ncl[i] = T.nco[i];
 }
 
 struct DemodTw {
@@ -293,21 +308,25 @@ __device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R
 
 // (int16_t)((double)q * 127.0) for q = RN(-re / ab1) and the same for im -- the
 // reference's soft bit (ofdm-decoder.cpp:188-189) -- without two IEEE divisions on the
-// common path.  q' = -re * rcp(ab1) is within 2 ulp of q, so x' = q' * 127 (float) is
-// within 3.8e-5 of the exact q * 127; truncation can differ only if x' lies within
-// that of a nonzero integer.  Those values (about 1 in 10^4) and operands outside the
-// reciprocal's comfortable range take the exact path: IEEE division, double product.
-__device__ __forceinline__ void soft_pair(float2 r1, float ab1, int &ir, int &ii) {
+// common path.  x' = re * (rcp(ab1) * -127) is within 127 * 2^-22 (rcp 1 ulp, two
+// roundings) + 127 * 2^-25 (the rounding of q itself) < D of the exact 127 q, so its
+// truncation (v_cvt_i32_f32 truncates) equals the reference's unless x' lies within D
+// of an integer.  Those values (about 1 in 10^4, zero included) and operands outside
+// the reciprocal's comfortable range take the exact path: IEEE division, double product.
+__device__ __forceinline__ bool soft_fast(float2 r1, float ab1, int &ir, int &ii) {
 #pragma clang fp contract(off)
-    constexpr float D = 0x1p-14f;                       // > 127 * 2^-22 + 2^-17 (q' and x' rounding)
-    const float inv = __builtin_amdgcn_rcpf(ab1);
-    const float xr = (-r1.x * inv) * 127.0f, xi = (-r1.y * inv) * 127.0f;
-    const float nr = rintf(xr), ni = rintf(xi);
-    const bool risky = (fabsf(xr - nr) < D && nr != 0.0f) || (fabsf(xi - ni) < D && ni != 0.0f) ||
-                       !(ab1 >= 0x1p-100f && ab1 <= 0x1p+100f);
-    ir = (int)truncf(xr);
-    ii = (int)truncf(xi);
-    if (risky) {
+    constexpr float D = 0x1p-14f;
+    const float m = __builtin_amdgcn_rcpf(ab1) * -127.0f;
+    const float xr = r1.x * m, xi = r1.y * m;
+    const float e = fminf(fabsf(xr - rintf(xr)), fabsf(xi - rintf(xi)));
+    // ab1 (>= 0 or NaN) outside [2^-100, 2^100]: one unsigned compare on its bits
+    const bool range = (__float_as_uint(ab1) - 0x0D800000u) > 0x64000000u;
+    ir = (int)xr;
+    ii = (int)xi;
+    return e < D || range;
+}
+__device__ __forceinline__ void soft_pair(float2 r1, float ab1, int &ir, int &ii) {
+    if (soft_fast(r1, ab1, ir, ii)) {
         ir = trunc127d(-r1.x / ab1);
         ii = trunc127d(-r1.y / ab1);
     }
@@ -324,13 +343,17 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                                                     OfdmTables T, int16_t *__restrict__ soft,
                                                     float *__restrict__ softf, float2 *__restrict__ fcpart,
                                                     DemodAux aux) {
-    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
-    __shared__ __attribute__((aligned(16))) uint32_t st[STG];
-    __shared__ float2 fcw[DT / 64];
+    __shared__ __attribute__((aligned(16))) float2 ex[2048 + 64 * (ZROW - 32)];
+    // the soft-bit stage and the FreqCorr partials reuse the FFT exchange buffer (after
+    // the FFT's last LDS pass, behind a barrier): 40 KB per workgroup with the NCO
+    // tables, so 4 workgroups per CU
+    uint32_t *st = (uint32_t *)ex;
+    float2 *fcw = ex;
+    static_assert(STG * 4 <= sizeof(ex), "stage fits the exchange buffer");
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x;
-    __shared__ double2 ncl[GEN ? NCO_N : 1];
+    __shared__ double2 ncl[GEN ? NCO_USED : 1];
     const DemodTw tw = tw_setup(twl, T, t);
     nco_setup<GEN>(ncl, T, t);
     __syncthreads();
@@ -387,31 +410,49 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     if (!ok && !skip && t == 0) atomicOr(T.err, KERR_FRAME);
     if (l0 <= NSYM && ok && !skip) {
         const int64_t dorg = fr.block0 + TU;           // first sample of segment B
-        // carriers of this thread's 8 bins (-1: none), two int16 per register
+        // LDS stage byte address of each of this thread's 8 bins (its carrier's slot, or
+        // the thread's dump slot K + t for a bin that carries nothing), two u16 per register
         uint32_t cb[4];
         {
             const int b0 = bin0_of(t);
+            auto slot = [&](int k3) -> uint32_t {
+#ifdef DEMOD_AB_NOPERM      // A/B timing only: bin-order LDS stage (no de-interleave scatter)
+                const int c = k3 < 6 ? k3 * DT + t : -1;
+#else
+                const int c = T.carrier_of_bin[b0 + 64 * k3];
+#endif
+                return (uint32_t)(c >= 0 ? c : K + t) * 4u;
+            };
 #pragma unroll
-            for (int k3 = 0; k3 < 8; k3 += 2)
-                cb[k3 >> 1] = (uint32_t)(uint16_t)T.carrier_of_bin[b0 + 64 * k3] |
-                              ((uint32_t)(uint16_t)T.carrier_of_bin[b0 + 64 * (k3 + 1)] << 16);
+            for (int k3 = 0; k3 < 8; k3 += 2) cb[k3 >> 1] = slot(k3) | (slot(k3 + 1) << 16);
         }
+        // the frame's samples and soft-bit rows through buffer descriptors (wave-uniform
+        // bases: 32-bit offsets, the 8 samples of a thread a scalar offset apart, no
+        // 64-bit address arithmetic per symbol)
+        const float2 *fb = s + fr.block0;
+        const __amdgpu_buffer_rsrc_t rin =
+            __builtin_amdgcn_make_buffer_rsrc((void *)fb, (short)0, (TU + NSYM * TS) * 8, 0x00020000);
+        int16_t *orow = soft + (int64_t)fr.out_slot * NSYM * SYMBITS;
+        const __amdgpu_buffer_rsrc_t rout =
+            __builtin_amdgcn_make_buffer_rsrc((void *)orow, (short)0, NSYM * SYMBITS * 2, 0x00020000);
+        auto ld = [&](int32_t off) -> float2 {                      // off: byte offset from block 0
+            return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0));
+        };
         float2 a[8], nx[8], P[8], ng6, ng7;
         // warm-up symbol l0 - 1 (block 0, the PRS, for the first chunk)
         {
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
+            const int32_t o = ((l0 - 1) * TS + t) * 8;
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = s[u + t + 256 * m];
+            for (int m = 0; m < 8; m++) a[m] = ld(o + 2048 * m);
             if (l0 == 1) mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
             else mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
         }
-        {
-            const int64_t u = fr.block0 + (int64_t)l0 * TS;
-            ng6 = s[u - 512 + t];
-            ng7 = s[u - 256 + t];
+        int32_t ov = (l0 * TS + t) * 8;                       // this thread's sample 0 of symbol l
+        ng6 = ld(ov - 4096);
+        ng7 = ld(ov - 2048);
 #pragma unroll
-            for (int m = 0; m < 8; m++) nx[m] = s[u + t + 256 * m];
-        }
+        for (int m = 0; m < 8; m++) nx[m] = ld(ov + 2048 * m);
         fft2048_wg(a, ex, tw, t);
         if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
             const int16_t v = snr_wg(a, t, red);
@@ -419,23 +460,48 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         }
 #pragma unroll
         for (int k = 0; k < 8; k++) P[k] = a[k];
+        // NCO of segment B: localPhase index of this thread's sample 0 of symbol l, stepped
+        // in 32 bits (-256 phase per register, -T_s phase per symbol, +512/+256 phase for
+        // the two guard samples); phase 0: oscillatorTable[lp_data] for every sample.  The
+        // three separately branched mixes keep the NCO's doubles out of the FFT's
+        // scheduling region (one region: the register allocator spills)
+        const float2 f0 = T.osc[fr.lp_data];
+        const int32_t ph = fr.phase_b;
+        // wave-uniform steps: SGPRs (readfirstlane), no VGPRs taken from the FFT
+        const int32_t d256 = __builtin_amdgcn_readfirstlane(nco_mod(256 * (int64_t)ph));
+        const int32_t dsym = __builtin_amdgcn_readfirstlane(nco_mod((int64_t)TS * ph));
+        const int32_t g512 = __builtin_amdgcn_readfirstlane(nco_mod(512 * (int64_t)ph)), g256 = d256;
+        int32_t ti = nco_index2(fr.lp_data, ph, fr.block0 + (int64_t)l0 * TS + t - dorg + 1);
         for (int l = l0; l < l1; l++) {
-            const int64_t u0 = fr.block0 + (int64_t)l * TS;
             // this symbol's samples and its guard samples, all loaded one symbol ahead
             // (a guard load issued here would expose a full HBM latency per symbol)
 #pragma unroll
             for (int m = 0; m < 8; m++) a[m] = nx[m];
             float2 g6 = ng6, g7 = ng7;
             if (l + 1 < l1) {
-                const int64_t u1 = u0 + TS;
-                ng6 = s[u1 - 512 + t];
-                ng7 = s[u1 - 256 + t];
+                const int32_t o1 = ov + TS * 8;
+                ng6 = ld(o1 - 4096);
+                ng7 = ld(o1 - 2048);
 #pragma unroll
-                for (int m = 0; m < 8; m++) nx[m] = s[u1 + t + 256 * m];
+                for (int m = 0; m < 8; m++) nx[m] = ld(o1 + 2048 * m);
             }
-            mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u0 + t, dorg);
-            g6 = mix1<GEN>(g6, T.osc, ncl, fr.lp_data, fr.phase_b, u0 - 512 + t, dorg);
-            g7 = mix1<GEN>(g7, T.osc, ncl, fr.lp_data, fr.phase_b, u0 - 256 + t, dorg);
+            ov += TS * 8;
+            if (!GEN || ph == 0) {
+#pragma unroll
+                for (int m = 0; m < 8; m++) a[m] = cmul_exact(a[m], f0);
+            } else {
+                int32_t x = ti;
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    a[m] = cmul_exact(a[m], nco_value(ncl, x));
+                    x = nco_sub(x, d256);
+                }
+            }
+            if (!GEN || ph == 0) g6 = cmul_exact(g6, f0);
+            else g6 = cmul_exact(g6, nco_value(ncl, nco_add(ti, g512)));
+            if (!GEN || ph == 0) g7 = cmul_exact(g7, f0);
+            else g7 = cmul_exact(g7, nco_value(ncl, nco_add(ti, g256)));
+            ti = nco_sub(ti, dsym);
             if (t >= 8) {                              // FreqCorr over i in [T_u, T_s)
                 const float2 p = cmul_conj_exact(a[6], g6);
                 fc.x += p.x; fc.y += p.y;
@@ -445,29 +511,65 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 fc.x += p.x; fc.y += p.y;
             }
             fft2048_wg(a, ex, tw, t);
-            float *sf = softf ? softf + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS : nullptr;
+            __syncthreads();                           // pass 3's reads of ex done: st reuses it
+            // DQPSK + soft bits of the 8 bins, fast path first; the few bins whose
+            // truncation the fast path cannot decide (soft_fast) are redone exactly after
+            // all 8 (one divergent branch per symbol instead of one per bin)
+            uint32_t risky = 0;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const float2 r1 = cmul_conj_exact(a[k], P[k]);
-                P[k] = a[k];
                 // ibits = (int16_t)(q * 127.0), q = -re / ab1 (IEEE float division) and
-                // ab1 = |re| + |im| (ofdm-decoder.cpp:185-189), computed exactly:
+                // ab1 = |re| + |im| (ofdm-decoder.cpp:185-189)
                 const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                 int ir, ii;
-                soft_pair(r1, ab1, ir, ii);
-                const int c = (int)(int16_t)((k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu));
-                st[c >= 0 ? c : K + t] = (uint32_t)(uint16_t)(int16_t)ir | ((uint32_t)(uint16_t)(int16_t)ii << 16);
-                if (sf && c >= 0) { sf[c] = -r1.x / ab1; sf[K + c] = -r1.y / ab1; }
+#ifdef DEMOD_AB_FASTSOFT    // A/B timing only (tools/build_variant.sh): no exactness check
+                { const float mm = __builtin_amdgcn_rcpf(ab1) * -127.0f; ir = (int)(r1.x * mm); ii = (int)(r1.y * mm); }
+#else
+                risky |= (uint32_t)soft_fast(r1, ab1, ir, ii) << k;
+#endif
+                const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
+                *(uint32_t *)((char *)st + addr) = __builtin_amdgcn_perm((uint32_t)ii, (uint32_t)ir, 0x05040100u);
             }
+            if (risky) {
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    if ((risky >> k) & 1u) {
+                        const float2 r1 = cmul_conj_exact(a[k], P[k]);
+                        const float ab1 = fabsf(r1.x) + fabsf(r1.y);
+                        const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
+                        *(uint32_t *)((char *)st + addr) = __builtin_amdgcn_perm(
+                            (uint32_t)trunc127d(-r1.y / ab1), (uint32_t)trunc127d(-r1.x / ab1), 0x05040100u);
+                    }
+                }
+            }
+            if (softf) {                               // parity tests only: the float soft values
+                float *sf = softf + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS;
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
+                    const int c = (int)(addr >> 2);
+                    if (c < K) {
+                        const float2 r1 = cmul_conj_exact(a[k], P[k]);
+                        const float ab1 = fabsf(r1.x) + fabsf(r1.y);
+                        sf[c] = -r1.x / ab1;
+                        sf[K + c] = -r1.y / ab1;
+                    }
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) P[k] = a[k];
             __syncthreads();
-            int16_t *row = soft + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS;
             // carriers 4q..4q+3, q < 384: re to row[4q..], im to row[K + 4q..]
+            const int32_t rowb = (l - 1) * SYMBITS * 2;
             for (int q = t; q < K / 4; q += DT) {
                 const uint4 w = ((const uint4 *)st)[q];
-                const uint2 re = make_uint2((w.x & 0xFFFFu) | (w.y << 16), (w.z & 0xFFFFu) | (w.w << 16));
-                const uint2 im = make_uint2((w.x >> 16) | (w.y & 0xFFFF0000u), (w.z >> 16) | (w.w & 0xFFFF0000u));
-                ((uint2 *)row)[q] = re;
-                ((uint2 *)(row + K))[q] = im;
+                const uint2 re = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x05040100u),
+                                            __builtin_amdgcn_perm(w.w, w.z, 0x05040100u));
+                const uint2 im = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x07060302u),
+                                            __builtin_amdgcn_perm(w.w, w.z, 0x07060302u));
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, re), rout, rowb + 8 * q, 0, 0);
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, im), rout, rowb + 2 * K + 8 * q, 0, 0);
             }
             __syncthreads();
         }
@@ -492,7 +594,7 @@ __global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, co
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x, f = blockIdx.x;
-    __shared__ double2 ncl[GEN ? NCO_N : 1];
+    __shared__ double2 ncl[GEN ? NCO_USED : 1];
     const DemodTw tw = tw_setup(twl, T, t);
     nco_setup<GEN>(ncl, T, t);
     __syncthreads();
@@ -533,7 +635,7 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
     __shared__ float val[2048];                          // |X| (method 0) or per-candidate sums
     __shared__ float cv[96];                             // method 1: correlationVector
     const int t = threadIdx.x, f = blockIdx.x;
-    __shared__ double2 ncl[GEN ? NCO_N : 1];
+    __shared__ double2 ncl[GEN ? NCO_USED : 1];
     const DemodTw tw = tw_setup(twl, T, t);
     nco_setup<GEN>(ncl, T, t);
     __syncthreads();
@@ -666,7 +768,7 @@ __global__ __launch_bounds__(DT) void k_symbol_wg(const float2 *__restrict__ smp
 
 // the kernels' NCO over a range of table indices (exhaustive parity check)
 __global__ __launch_bounds__(DT) void k_nco_eval(OfdmTables T, int32_t first, int32_t n, float2 *__restrict__ out) {
-    __shared__ double2 ncl[NCO_N];
+    __shared__ double2 ncl[NCO_USED];
     nco_setup<true>(ncl, T, threadIdx.x);
     __syncthreads();
     for (int32_t i = blockIdx.x * DT + threadIdx.x; i < n; i += gridDim.x * DT) out[i] = nco_value(ncl, first + i);

@@ -8,7 +8,8 @@ OUT=$P/build/variant_$1
 mkdir -p "$OUT" "$P/lib/variants"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -w $2"
 for f in k_ofdm.hip k_demod.hip k_viterbi.hip k_dabplus.hip dabgpu_host.cpp; do
-    /opt/rocm/bin/hipcc $FLAGS -x hip -c "$P/csrc/$f" -o "$OUT/$f.o" &
+    extra=""; [ "$f" = k_demod.hip ] && extra="-fno-slp-vectorize"    # as the Makefile
+    /opt/rocm/bin/hipcc $FLAGS $extra -x hip -c "$P/csrc/$f" -o "$OUT/$f.o" &
 done
 wait
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$P/lib/variants/libdabgpu_$1.so" "$OUT"/*.o

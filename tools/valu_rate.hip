@@ -1,6 +1,7 @@
 // valu_rate.hip -- calibration microbenchmark (not part of the product): sustained
 // wave64 VALU issue rate per SIMD on this GPU for the instruction classes k_acs uses
-// (32-bit add, packed 16-bit add/min, DPP move, 16-bit compare into a lane mask).
+// (32-bit add, packed 16-bit add/min, DPP move, 16-bit compare into a lane mask) and
+// the float kinds the demod uses (f32, packed f32, f64).
 // Grid: 32 waves per CU (8 per SIMD), each with 8 independent dependency chains.
 // Prints cycles per wave-instruction per SIMD (2.0 = full rate of a SIMD-32).
 #include <hip/hip_runtime.h>
@@ -25,6 +26,11 @@ __global__ __launch_bounds__(64) void k_rate(uint32_t *out, int iters) {
                 else if constexpr (OP == 2) asm volatile("v_mov_b32_dpp %0, %0 quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf" : "+v"(v[c]));
                 else if constexpr (OP == 3) asm volatile("v_pk_min_u16 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
                 else if constexpr (OP == 4) asm volatile("v_cmp_gt_u16_sdwa vcc, %0, %1 src0_sel:WORD_1 src1_sel:WORD_1" :: "v"(v[c]), "v"(k1) : "vcc");
+                else if constexpr (OP == 5) asm volatile("v_add_f32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 6) asm volatile("v_fmac_f32 %0, %1, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 7) asm volatile("v_rcp_f32 %0, %0" : "+v"(v[c]));
+                else if constexpr (OP == 8) asm volatile("v_rndne_f32 %0, %0" : "+v"(v[c]));
+                else if constexpr (OP == 9) asm volatile("v_cvt_i32_f32 %0, %0" : "+v"(v[c]));
             }
         }
     }
@@ -34,17 +40,49 @@ __global__ __launch_bounds__(64) void k_rate(uint32_t *out, int iters) {
     out[blockIdx.x * 64 + threadIdx.x] = s;
 }
 
+// the same for 64-bit operands (register pairs): packed f32 and f64
 template <int OP>
+__global__ __launch_bounds__(64) void k_rate64(uint64_t *out, int iters) {
+    uint64_t v[8];
+    const uint64_t k1 = threadIdx.x * 7 + 1;
+#pragma unroll
+    for (int c = 0; c < 8; c++) v[c] = threadIdx.x * 13 + c;
+    for (int it = 0; it < iters; it++) {
+#pragma unroll
+        for (int r = 0; r < 16; r++) {
+#pragma unroll
+            for (int c = 0; c < 8; c++) {
+                if constexpr (OP == 0) asm volatile("v_pk_add_f32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 1) asm volatile("v_pk_fma_f32 %0, %0, %1, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 2) asm volatile("v_pk_mul_f32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 3) asm volatile("v_fma_f64 %0, %0, %1, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 4) asm volatile("v_mul_f64 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 5) asm volatile("v_add_f64 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+            }
+        }
+    }
+    uint64_t s = 0;
+#pragma unroll
+    for (int c = 0; c < 8; c++) s ^= v[c];
+    out[blockIdx.x * 64 + threadIdx.x] = s;
+}
+
+template <int OP, bool W64 = false>
 static void run(const char *name, int cus) {
     const int waves = cus * 32, iters = 2000;
-    uint32_t *d;
-    CK(hipMalloc(&d, sizeof(uint32_t) * waves * 64));
+    uint64_t *d;
+    CK(hipMalloc(&d, sizeof(uint64_t) * waves * 64));
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    hipLaunchKernelGGL(k_rate<OP>, dim3(waves), dim3(64), 0, 0, d, 10);
+    auto launch = [&](int it) {
+        if constexpr (W64) hipLaunchKernelGGL(k_rate64<OP>, dim3(waves), dim3(64), 0, 0, d, it);
+        else hipLaunchKernelGGL(k_rate<OP>, dim3(waves), dim3(64), 0, 0, (uint32_t *)d, it);
+    };
+    for (int w = 0; w < 20; w++) launch(200);      // clocks up
+    launch(10);
     hipEventRecord(a);
-    hipLaunchKernelGGL(k_rate<OP>, dim3(waves), dim3(64), 0, 0, d, iters);
+    launch(iters);
     hipEventRecord(b);
     hipEventSynchronize(b);
     float ms = 0;
@@ -66,5 +104,16 @@ int main() {
     run<2>("v_mov_b32_dpp quad_perm", cus);
     run<3>("v_pk_min_u16", cus);
     run<4>("v_cmp_gt_u16_sdwa", cus);
+    run<5>("v_add_f32", cus);
+    run<6>("v_fmac_f32", cus);
+    run<7>("v_rcp_f32", cus);
+    run<8>("v_rndne_f32", cus);
+    run<9>("v_cvt_i32_f32", cus);
+    run<0, true>("v_pk_add_f32", cus);
+    run<1, true>("v_pk_fma_f32", cus);
+    run<2, true>("v_pk_mul_f32", cus);
+    run<3, true>("v_fma_f64", cus);
+    run<4, true>("v_mul_f64", cus);
+    run<5, true>("v_add_f64", cus);
     return 0;
 }
