@@ -313,7 +313,9 @@ def main():
     ap.add_argument("--frames", type=int, default=24,
                     help="frames per ensemble per step (the pipeline's batch: 24 frames = 2.3 s of air time; "
                          "throughput saturates from ~24 on MI355X, profiles/r01_frames_sweep.txt)")
-    ap.add_argument("--cfo", type=float, default=0.0, help="carrier frequency offset of the synthetic IQ (Hz)")
+    ap.add_argument("--cfo", type=float, default=1300.0,
+                    help="carrier frequency offset of the synthetic IQ (Hz); nonzero by default: a receiver's NCO "
+                         "always runs (phase = coarse + fine correction), 0 takes the constant-phase shortcut")
     ap.add_argument("--iq-source", choices=["local", "rccl"], default="local")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)

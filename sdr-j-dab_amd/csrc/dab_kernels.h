@@ -115,7 +115,8 @@ struct VitJob {
 
 // DAB+ superframe layer (k_dabplus.hip)
 constexpr int DP_MAX_RS = 48;       // RSDims = bitRate / 8, bitRate <= 384
-constexpr int DP_TAB_BYTES = 256 + 256 + 512 + 2560 + 512 + 2048;   // GF exp/log, fire, mul[10], crc, pow8
+constexpr int DP_TAB_BYTES = 256 + 256 + 512 + 2560 + 512 + 2048 + 516;   // GF exp/log, fire, mul[10], crc, pow8, fibcrc
+constexpr int FIBCRC_OFF = 256 + 256 + 512 + 2560 + 512 + 2048;   // uint16 bit contribution[256] + init effect
 struct DpState {
     int32_t fill, blocks;           // blockFillIndex, blocksInBuffer (mp4processor.cpp:86-87)
 };
@@ -154,7 +155,8 @@ hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
 hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
-hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib, const int32_t *slots = nullptr);
+hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib, const uint8_t *tabs,
+                           const int32_t *slots = nullptr);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
 hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_t n_values, float *dst);
 hipError_t launch_rs(hipStream_t st, const uint8_t *in, int n, const uint8_t *tabs, uint8_t *out, int16_t *ret);

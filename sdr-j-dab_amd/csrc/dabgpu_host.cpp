@@ -170,6 +170,20 @@ struct HostTables {
         pow8[0] = 1;
         for (int d = 1; d < 1024; d++)
             pow8[d] = (uint16_t)(((uint32_t)pow8[d - 1] << 8) ^ crc[pow8[d - 1] >> 8]);
+        // FIB CRC (dab-constants.h:310-340) by linearity: the register after 256 bits is
+        // the XOR of each 1 bit's contribution (a lone 1 at position i, zeros after) and
+        // of the all-ones initial value's (256 zero bits): k_fic_post reduces it over a wave
+        uint16_t *fc = (uint16_t *)(dptab.data() + FIBCRC_OFF);
+        auto run = [](uint32_t r, int one_at) {
+            for (int i = 0; i < 256; i++) {
+                const uint32_t top = (r >> 15) & 1u;
+                r = (r << 1) & 0xFFFFu;
+                if (top ^ (uint32_t)(i == one_at)) r ^= 0x1021u;
+            }
+            return (uint16_t)r;
+        };
+        for (int i = 0; i < 256; i++) fc[i] = run(0, i);
+        fc[256] = run(0xFFFF, -1);
     }
     std::vector<uint8_t> dptab;             // GF exp[256], log[256], fire uint16[256]
 };
@@ -613,7 +627,7 @@ static int fic_common(dabgpu_ctx *c, VitJob &J, uint8_t *bits, uint8_t *ok) {
     J.out_stride = 768;
     J.prbs = 1;
     if ((rc = run_viterbi(c, J, 768))) return rc;
-    if (ok) HIPCHK(launch_fic_post(c->stream, bits, ok, 3 * J.n_cw));
+    if (ok) HIPCHK(launch_fic_post(c->stream, bits, ok, 3 * J.n_cw, c->dptab));
     return 0;
 }
 
@@ -1394,12 +1408,12 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, slots_d));
+        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
     } else if (fic_bits) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
         HIPCHK(launch_viterbi(bs, JF));
-        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, slots_d));
+        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
         HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
     } else if (do_msc) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));

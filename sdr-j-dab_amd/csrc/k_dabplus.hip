@@ -30,7 +30,7 @@ struct GfTabs {
     uint16_t crc[256];       // CRC-CCITT (0x1021, msb first) byte table
     uint16_t pow8[1024];     // x^(8d) mod the CRC polynomial
 };
-static_assert(sizeof(GfTabs) == DP_TAB_BYTES, "host table layout");
+static_assert(sizeof(GfTabs) == FIBCRC_OFF, "host table layout (the FIB CRC table follows)");
 
 __device__ __forceinline__ int gmul(const GfTabs &g, int a, int b) {
     return (a && b) ? g.exp[mod255(g.log[a] + g.log[b])] : 0;
@@ -261,7 +261,7 @@ __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
         if (lane == 0) *code = 0;
         return;
     }
-    for (int i = lane; i < DP_TAB_BYTES / 4; i += 64)
+    for (int i = lane; i < (int)sizeof(GfTabs) / 4; i += 64)
         if (i < fire0 || i >= fire1) ((uint32_t *)&g)[i] = tabs32[i];
     for (int p = 11 + lane; p < fsz; p += 64) sfb[p] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, p);
     for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;

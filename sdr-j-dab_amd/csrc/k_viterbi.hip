@@ -407,7 +407,9 @@ __device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&ro
 template <int NP> struct AcsLds {
     uint32_t bm[NP * 8 * BRS];
     int32_t rowoff[2 * NP][16];
+    int2 ro2[NP][16];               // SRC_MSC pair: both codewords' row byte offsets per idx & 15
 };
+constexpr int32_t RO_EMPTY = 0x40000000;   // byte offset past any ring: the buffer load returns 0
 template <int KIND, int NP>
 __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) {
     uint32_t *bm = L.bm;
@@ -421,6 +423,20 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         any = any || c[k].valid;
     }
     if (!any) return;
+    if constexpr (KIND == SRC_MSC) {
+        // the pair's two delay-line row tables side by side, in bytes, an empty row (or
+        // an invalid codeword's) as an offset past the buffer: one LDS read and no
+        // compare per soft value pair in the tile loader
+        if (lane < 16) {
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                const int32_t a = rowoff[2 * p][lane], b = rowoff[2 * p + 1][lane];
+                L.ro2[p][lane] = make_int2(a >= 0 && c[2 * p].valid ? 2 * a : RO_EMPTY,
+                                           b >= 0 && c[2 * p + 1].valid ? 2 * b : RO_EMPTY);
+            }
+        }
+        wave_sync();
+    }
     // profiles are wave-uniform: scalar loads, kept out of the vector memory queue
     const ProfR p0 = prof_regs(J.prof + c[0].prof);
     bool same = true;
@@ -479,6 +495,23 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         } else {
             i0[0] = i0[1] = i0[2] = i0[3] = 0;
         }
+        if constexpr (KIND == SRC_MSC) {
+            if (same) {
+#pragma unroll
+                for (int p = 0; p < NP; p++) {
+                    const uint32_t ka = t < stp[2 * p] ? k0 : 0u, kb = t < stp[2 * p + 1] ? k0 : 0u;
+#pragma unroll
+                    for (int e = 0; e < 4; e++) {
+                        const int2 r = L.ro2[p][i0[e] & 15];
+                        const int32_t oa = ((ka >> e) & 1u) ? r.x + 2 * i0[e] : RO_EMPTY;
+                        const int32_t ob = ((kb >> e) & 1u) ? r.y + 2 * i0[e] : RO_EMPTY;
+                        s[p][e][0] = __builtin_amdgcn_raw_buffer_load_b16(c[2 * p].rs, oa, 0, 0);
+                        s[p][e][1] = __builtin_amdgcn_raw_buffer_load_b16(c[2 * p + 1].rs, ob, 0, 0);
+                    }
+                }
+                return;
+            }
+        }
         sfor<0, 2 * NP>([&](auto kc) {
             constexpr int k = decltype(kc)::value;
             int ik[4];
@@ -504,7 +537,9 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     for (int t0 = 0; t0 < steps; t0 += VT) {
         if (mine) put();
         wave_sync();
+#ifndef ACS_AB_NOLOAD      // A/B timing only (tools/build_variant.sh): tiles reuse the first inputs
         fetch(t0 + VT, mine ? t0 + VT + lane : steps);
+#endif
         for (int u = 0; u < 2; u++) {
             const int tw = t0 + u * WS;
             if (tw >= steps) break;
@@ -750,25 +785,35 @@ __global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) 
 }
 
 // FIB CRC check (dab-constants.h:310-340): invert the 16 CRC bits in place, run
-// CRC-CCITT from all-ones over 256 bits, pass iff the register ends at zero.
+// CRC-CCITT from all-ones over 256 bits, pass iff the register ends at zero.  The CRC is
+// linear, so one wave per FIB: lane l takes bits 4l..4l+3 (one coalesced 4-byte load),
+// XORs the contributions of its 1 bits (host table, FIBCRC_OFF) and the wave XOR-reduces.
+// No LDS allocation: the kernel runs beside the next run's demod, whose workgroups hold
+// all of a CU's LDS (the 512-byte table is read through the caches instead).
 // slots (optional): ring slot per frame (12 FIBs), < 0 = frame not committed: no check, ok = 0
-__global__ void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok, int n_fib,
-                           const int32_t *__restrict__ slots) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+__global__ __launch_bounds__(256) void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok, int n_fib,
+                                                  const int32_t *__restrict__ slots,
+                                                  const uint16_t *__restrict__ tab) {
+    const int lane = threadIdx.x & 63;
+    const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (f >= n_fib) return;
     if (slots && slots[f / 12] < 0) {
-        ok[f] = 0;
+        if (lane == 0) ok[f] = 0;
         return;
     }
-    uint8_t *b = bits + (int64_t)f * 256;
-    for (int i = 240; i < 256; i++) b[i] ^= 1;
-    uint32_t r = 0xFFFF;
-    for (int i = 0; i < 256; i++) {
-        const uint32_t top = (r >> 15) & 1u;
-        r = (r << 1) & 0xFFFFu;
-        if (top ^ b[i]) r ^= 0x1021u;
+    uint32_t *w = (uint32_t *)(bits + (int64_t)f * 256) + lane;
+    uint32_t v = *w;
+    if (lane >= 60) {                                    // bits 240..255: the CRC, inverted
+        v ^= 0x01010101u;
+        *w = v;
     }
-    ok[f] = r == 0;
+    uint32_t r = 0;
+#pragma unroll
+    for (int e = 0; e < 4; e++)
+        if ((v >> (8 * e)) & 0xFFu) r ^= tab[4 * lane + e];
+#pragma unroll
+    for (int o = 32; o; o >>= 1) r ^= (uint32_t)__shfl_xor((int)r, o, 64);
+    if (lane == 0) ok[f] = (r ^ tab[256]) == 0;
 }
 
 template <template <int> class K>
@@ -818,9 +863,11 @@ hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJo
     return hipGetLastError();
 }
 
-hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib, const int32_t *slots) {
+hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib, const uint8_t *tabs,
+                           const int32_t *slots) {
     if (n_fib <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_fic_post, dim3((n_fib + 63) / 64), dim3(64), 0, st, bits, ok, n_fib, slots);
+    hipLaunchKernelGGL(k_fic_post, dim3((n_fib + 3) / 4), dim3(256), 0, st, bits, ok, n_fib, slots,
+                       (const uint16_t *)(tabs + FIBCRC_OFF));
     return hipGetLastError();
 }
 
