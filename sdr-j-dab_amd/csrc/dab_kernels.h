@@ -60,12 +60,18 @@ struct AcqResult {
 
 // ---- Viterbi ------------------------------------------------------------
 // decision words: per chunk of DEC_WORD_STEPS trellis steps and codeword row, 64
-// lanes x 32 bits (k_viterbi.hip: dec[(chunk * dec_ncw + row) * 64 + lane]); rows
-// padded to a whole traceback wave of 64
+// lanes x 32 bits, in blocks of 64 rows (one traceback wave) whose chunks are
+// contiguous: dec[((row / 64 * dec_nch + chunk) * 64 + row % 64) * 64 + lane]
+// (dec_word_index); rows padded to a whole block of 64
 constexpr int DEC_WORD_STEPS = 30;
 inline __host__ __device__ int64_t dec_rows(int n_cw) { return ((int64_t)n_cw + 63) / 64 * 64; }
+inline __host__ __device__ int32_t dec_chunks(int nbits) { return (nbits + 6 + DEC_WORD_STEPS - 1) / DEC_WORD_STEPS; }
 inline __host__ __device__ int64_t dec_bytes(int n_cw, int nbits) {
-    return (int64_t)((nbits + 6 + DEC_WORD_STEPS - 1) / DEC_WORD_STEPS) * dec_rows(n_cw) * 64 * 4;
+    return (int64_t)dec_chunks(nbits) * dec_rows(n_cw) * 64 * 4;
+}
+// first word of (row, chunk 0); chunk c of the row is 4096 words further on
+inline __host__ __device__ int64_t dec_word_index(int64_t row, int32_t nch) {
+    return ((row >> 6) * nch * 64 + (row & 63)) * 64;
 }
 
 // depuncturing profile: up to 4 (L_i, PI_i) segments + the 24-bit PI_X tail
@@ -106,6 +112,7 @@ struct VitJob {
     // outputs
     uint32_t *dec;                  // decision words (dec_bytes(n_cw, max nbits) bytes)
     int64_t dec_ncw;                // rows of the decision buffer: >= dec_rows(n_cw)
+    int32_t dec_nch;                // chunks per row: dec_chunks(max nbits)
     uint8_t *out;
     int64_t out_stride;             // bytes per codeword
     int32_t prbs;                   // xor energy-dispersal sequence

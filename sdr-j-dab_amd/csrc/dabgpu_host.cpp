@@ -587,6 +587,7 @@ static int run_viterbi(dabgpu_ctx *c, VitJob &J, int max_nbits) {
     if (rc) return rc;
     J.dec = (uint32_t *)dec;
     J.dec_ncw = dec_rows(J.n_cw);
+    J.dec_nch = dec_chunks(max_nbits);
     J.prbs_words = c->prbs;
     J.err = c->err;
     HIPCHK(launch_viterbi(c->stream, J));
@@ -1379,6 +1380,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         JF.prbs_words = c->prbs;
         JF.dec = p->dec_d[par] + p->dec_fic_off;
         JF.dec_ncw = dec_rows(JF.n_cw);
+        JF.dec_nch = dec_chunks(768);
     }
     if (do_msc) {
         JM.kind = SRC_MSC;
@@ -1399,6 +1401,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         JM.prbs_words = c->prbs;
         JM.dec = p->dec_d[par];
         JM.dec_ncw = dec_rows(JM.n_cw);
+        JM.dec_nch = dec_chunks(p->max_nbits);
     }
     if (fic_bits && do_msc) {
         HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));

@@ -31,8 +31,10 @@
 //               the lane that held the traced state, two steps per LDS round trip.
 //               Bits leave through 2-B stores with the energy-dispersal PRBS xor-ed in.
 //
-// Decision layout: dec[(chunk * dec_ncw + row) * 64 + lane] (uint32), bit k =
-// decision of `lane` at trellis step 30*chunk + k (k < 30).
+// Decision layout (dab_kernels.h dec_word_index): 64-row blocks, each block's chunks
+// contiguous (a codeword's words then lie within 1.7 MB instead of one per 14 MB stride,
+// which cost the ACS its TLB reach), word [lane] of (row, chunk): bit k = decision of
+// `lane` at trellis step 30*chunk + k (k < 30).
 #include "dab_device.h"
 #include "dab_kernels.h"
 #include <algorithm>
@@ -358,8 +360,8 @@ __device__ __forceinline__ uint32_t renorm(uint32_t x) {
 // they shift down their half of w (dec_in), 15 steps per half-word, and are
 // unpacked to one word per codeword (step k at bit k) at the end of the word.
 template <int NP, bool FULL>
-__device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
-                                         uint32_t *dec, const int64_t (&rb)[2 * NP], int64_t o, int lane) {
+__device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
+                                            uint32_t (&cw)[2 * NP]) {
     static_assert(WS == 30, "two 15-step half-words per decision word");
     // the 6 per-phase row addresses once per word: each step's read is then one
     // ds_read_b64 at an immediate offset
@@ -395,11 +397,27 @@ __device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&ro
     for (int p = 0; p < NP; p++) {
         const uint32_t c0 = ((w0[p] >> 1) & 0x7FFFu) | ((w[p] << 14) & 0x3FFF8000u);
         const uint32_t c1 = ((w0[p] >> 17) & 0x7FFFu) | ((w[p] >> 2) & 0x3FFF8000u);
-        if (rb[2 * p] >= 0) (dec + rb[2 * p] + o)[lane] = c0;
-        if (rb[2 * p + 1] >= 0) (dec + rb[2 * p + 1] + o)[lane] = c1;
+        cw[2 * p] = c0;
+        cw[2 * p + 1] = c1;
     }
 #pragma unroll
     for (int p = 0; p < NP; p++) x[p] = renorm(x[p]);
+}
+// ... and its words stored at chunk offset o (rb[k] < 0: codeword k not stored)
+// (through a buffer descriptor: the word's 32-bit offset is wave-uniform, so the store
+// carries one lane offset register instead of a 64-bit address per lane)
+template <int NP, bool FULL>
+__device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
+                                         __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP], int64_t o, int lane) {
+    uint32_t cw[2 * NP];
+    acs_word_cw<NP, FULL>(bm, row, x, nst, cw);
+#pragma unroll
+    for (int k = 0; k < 2 * NP; k++)
+        if (rb[k] >= 0)
+#ifdef ACS_AB_NODEC          // A/B timing only: decisions not written (cost of the decision traffic)
+            if ((cw[k] ^ (uint32_t)o) == 0xDEADBEEFu)
+#endif
+            __builtin_amdgcn_raw_buffer_store_b32(cw[k], drs, 4 * lane, (int)(4 * (rb[k] + o)), 0);
 }
 
 // NP pairs of codewords per wave: codewords 2*NP*w .. 2*NP*w + 2*NP - 1 (logical order).
@@ -444,9 +462,12 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++) {
         same = same && c[k].prof == c[0].prof;
-        stp[k] = c[k].valid ? __builtin_amdgcn_readfirstlane(J.prof[c[k].prof].nbits) + 6 : 0;
+        // wave-uniform by construction; readfirstlane keeps the tile/word loops scalar
+        // (a step count in a VGPR turns every loop exit into exec-mask juggling)
+        stp[k] = __builtin_amdgcn_readfirstlane(c[k].valid ? J.prof[c[k].prof].nbits + 6 : 0);
         steps = max(steps, stp[k]);
     }
+    same = __builtin_amdgcn_readfirstlane((int)same) != 0;
     // per-lane LDS row of each relabelling phase (see header): q = output pattern of
     // butterfly i = rotl6(lane, r) & 31; upper lanes of a pair swap the two rows
     uint32_t row[6];
@@ -463,9 +484,10 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     for (int p = 0; p < NP; p++) x[p] = lane == 0 ? 0u : 0x003F003Fu;   // viterbi.cpp:360-371
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++) {
-        rb[k] = c[k].valid ? (int64_t)c[k].row * 64 : -1;
+        rb[k] = c[k].valid ? dec_word_index(c[k].row, J.dec_nch) : -1;
     }
-    const int64_t cstride = J.dec_ncw * 64;
+    const int64_t cstride = 64 * 64;                    // words per chunk of a 64-row block
+    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc((void *)J.dec, (short)0, -1, 0x00020000);
     // inputs of the next tile are loaded while the current one runs its ACS;
     // lane < VT handles step t0 + lane
     u16x2 s[NP][4];                                      // packed {A, B} soft values, per pair
@@ -544,8 +566,8 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
             const int tw = t0 + u * WS;
             if (tw >= steps) break;
             const int64_t o = (int64_t)(tw / WS) * cstride;
-            if (tw + WS <= steps) acs_word<NP, true>(bm + 2 * WS * u, row, x, WS, J.dec, rb, o, lane);
-            else acs_word<NP, false>(bm + 2 * WS * u, row, x, steps - tw, J.dec, rb, o, lane);
+            if (tw + WS <= steps) acs_word<NP, true>(bm + 2 * WS * u, row, x, WS, drs, rb, o, lane);
+            else acs_word<NP, false>(bm + 2 * WS * u, row, x, steps - tw, drs, rb, o, lane);
         }
         wave_sync();
     }
@@ -626,8 +648,9 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
         for (int i = lane; i < nw; i += 64) prbs_l[i] = J.prbs_words[i];
         wave_sync();
     }
-    const uint32_t *blk0 = J.dec + (int64_t)blk * TB_CW * 64;
-    const int64_t cstride = J.dec_ncw * 64;
+    static_assert(TB_CW == 64, "a traceback wave is one 64-row block of the decision layout");
+    const uint32_t *blk0 = J.dec + dec_word_index((int64_t)blk * TB_CW, J.dec_nch);
+    const int64_t cstride = 64 * 64;
     int lr = 0;                                          // lane index holding the traced state
     // decision chunks stream in through a 3-deep register ring (2 chunks = 32 KB per
     // wave in flight while one is walked): the walk itself is short, the loads are not
@@ -836,12 +859,12 @@ template <int KIND> struct TbK { static auto fn() { return k_traceback<KIND>; } 
 // DPP hazards and LDS latency better than instruction-level parallelism here.
 hipError_t launch_acs(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
-    if (job.dec_ncw < dec_rows(job.n_cw)) return hipErrorInvalidValue;
+    if (job.dec_ncw < dec_rows(job.n_cw) || job.dec_nch <= 0) return hipErrorInvalidValue;
     return launch_kind<AcsK>(st, job, dim3((job.n_cw + 1) / 2));
 }
 hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
-    if (job.dec_ncw < dec_rows(job.n_cw)) return hipErrorInvalidValue;
+    if (job.dec_ncw < dec_rows(job.n_cw) || job.dec_nch <= 0) return hipErrorInvalidValue;
     return launch_kind<TbK>(st, job, dim3((job.n_cw + TB_CW - 1) / TB_CW));
 }
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
@@ -851,7 +874,8 @@ hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
 // MSC (a) and FIC (b) decoded by one ACS launch and one traceback launch
 hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
-    if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw)) return hipErrorInvalidValue;
+    if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw) || a.dec_nch <= 0 || b.dec_nch <= 0)
+        return hipErrorInvalidValue;
     const int nwa = (a.n_cw + 1) / 2, nwb = (b.n_cw + 1) / 2;
     hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
     return hipGetLastError();
