@@ -8,6 +8,7 @@
 #include <cstring>
 #include <cstdarg>
 #include <string>
+#include <functional>
 #include <vector>
 #include <mutex>
 #include <algorithm>
@@ -766,6 +767,15 @@ struct dabgpu_pipe {
     int32_t *h_si = nullptr;
     float2 *h_fc = nullptr;
     int16_t *h_snr = nullptr;
+    // pinned staging of the back end's per-run uploads (CIF counters, FIC slots), one
+    // half per back-end stream; ev_copy[par] marks the uploads done before reuse
+    int64_t *h_cif0 = nullptr;
+    int32_t *h_ncif = nullptr, *h_slots = nullptr;
+    hipEvent_t ev_copy[2] = {nullptr, nullptr};
+    bool copy_rec[2] = {false, false};
+    // speculative back end (dabgpu_pipe_run): queued behind the first front pass
+    bool speculate = true;                      // env DABGPU_NO_SPECULATE=1: off (A/B)
+    int64_t front_launches = 0, spec_runs = 0, spec_hits = 0;
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
     std::vector<int32_t> last_si;
@@ -884,8 +894,12 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     if (!rc && (hipHostMalloc((void **)&p->h_frames, sizeof(dabgpu_frame) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_si, sizeof(int32_t) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_fc, sizeof(float2) * SF, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&p->h_snr, sizeof(int16_t) * SF, hipHostMallocDefault) != hipSuccess))
+                hipHostMalloc((void **)&p->h_snr, sizeof(int16_t) * SF, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_cif0, sizeof(int64_t) * p->S * 2, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_ncif, sizeof(int32_t) * p->S * 2, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_slots, sizeof(int32_t) * SF * 2, hipHostMallocDefault) != hipSuccess))
         rc = fail(DABGPU_E_NOMEM, "pipe pinned staging");
+    if (const char *e = getenv("DABGPU_NO_SPECULATE")) p->speculate = !(e[0] == '1');
     A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
     A((void **)&p->cif0_d, sizeof(int64_t) * p->S * 2);
     A((void **)&p->ncif_d, sizeof(int32_t) * p->S * 2);
@@ -903,7 +917,9 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
                 hipEventCreateWithFlags(&p->ev_dp, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_front, hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_back[0], hipEventDisableTiming) != hipSuccess ||
-                hipEventCreateWithFlags(&p->ev_back[1], hipEventDisableTiming) != hipSuccess))
+                hipEventCreateWithFlags(&p->ev_back[1], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_copy[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_copy[1], hipEventDisableTiming) != hipSuccess))
         rc = fail(DABGPU_E_HIP, "pipe stream/event create failed");
     if (!rc) {
         const Profile fp = fic_profile();
@@ -956,11 +972,12 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     (void)hipStreamSynchronize(p->c->stream);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamSynchronize(v);
     for (auto e : p->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1], p->ev_dp})
+    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1], p->ev_dp, p->ev_copy[0], p->ev_copy[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
-    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr})
+    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_cif0,
+                    (void *)p->h_ncif, (void *)p->h_slots})
         if (h) (void)hipHostFree(h);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
@@ -1041,7 +1058,8 @@ extern "C" int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq, int64_t stri
 // host with the measured values and commits the longest correctly predicted
 // prefix of each stream (ofdm-processor.cpp:344-468).
 static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
-                           std::vector<int> &done, std::vector<StreamSt> &cur, bool &progress, bool &lost) {
+                           std::vector<int> &done, std::vector<StreamSt> &cur, bool &progress, bool &lost,
+                           const std::function<int()> &after_launch = nullptr) {
     dabgpu_ctx *c = p->c;
     const int S = p->S, F = p->F;
     std::vector<dabgpu_frame> fr;
@@ -1103,6 +1121,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     // correction first: findIndex, block 0 and the demod run as three launches.
     bool fast = true;
     for (const dabgpu_frame &d : fr) fast = fast && !(d.flags & 1);
+    p->front_launches++;
     memcpy(p->h_frames, fr.data(), sizeof(dabgpu_frame) * n);
     HIPCHK(hipMemcpyAsync(p->frames_d, p->h_frames, sizeof(dabgpu_frame) * n, hipMemcpyHostToDevice, c->stream));
     std::vector<int32_t> si(n);
@@ -1128,6 +1147,8 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
     }
     HIPCHK(hipMemcpyAsync(p->h_si, p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
+    if (after_launch)
+        if (int rc = after_launch()) return rc;
     if (int rc = kernel_errors(c)) return rc;
     memcpy(si.data(), p->h_si, sizeof(int32_t) * n);
     if (fast) {
@@ -1319,6 +1340,124 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     if (p->back_rec[par]) HIPCHK(hipStreamWaitEvent(c->stream, p->ev_back[par], 0));
     std::vector<int> done(S, 0);
     std::vector<StreamSt> cur = p->st;
+    p->cur = par;
+    hipStream_t bs = p->vs[par];
+    // Channel decoding on the pipeline's back-end stream, after this run's front end:
+    // FIC for every committed frame (slot[s*F+f] = its ring slot, -1 none), MSC for all
+    // subchannels of every delivered CIF (dn[s] frames of stream s).  With both, one ACS
+    // and one traceback launch decode them together (the FIC's short waves fill the SIMDs
+    // the MSC's last waves leave idle); decisions in separate halves of the stream's
+    // decision buffer.
+    auto enqueue_back = [&](const std::vector<int> &dn, const std::vector<int32_t> &slots) -> int {
+        HIPCHK(hipEventRecord(p->ev_front, c->stream));
+        HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
+        // per stream: CIF index of its first CIF slot and the CIFs it delivered (the
+        // staging half is reused only once its previous uploads have executed)
+        if (p->copy_rec[par]) HIPCHK(hipEventSynchronize(p->ev_copy[par]));
+        for (int s = 0; s < S; s++) {
+            p->h_cif0[(size_t)par * S + s] = p->st[s].cif_count;
+            p->h_ncif[(size_t)par * S + s] = 4 * dn[s];
+        }
+        HIPCHK(hipMemcpyAsync(p->cif0_d + (size_t)par * S, p->h_cif0 + (size_t)par * S, sizeof(int64_t) * S,
+                              hipMemcpyHostToDevice, bs));
+        HIPCHK(hipMemcpyAsync(p->ncif_d + (size_t)par * S, p->h_ncif + (size_t)par * S, sizeof(int32_t) * S,
+                              hipMemcpyHostToDevice, bs));
+        VitJob JF, JM;
+        memset(&JF, 0, sizeof JF);
+        memset(&JM, 0, sizeof JM);
+        int32_t *slots_d = p->slots_d + (size_t)par * S * F;
+        if (fic_bits) {
+            memcpy(p->h_slots + (size_t)par * S * F, slots.data(), sizeof(int32_t) * S * F);
+            HIPCHK(hipMemcpyAsync(slots_d, p->h_slots + (size_t)par * S * F, sizeof(int32_t) * S * F,
+                                  hipMemcpyHostToDevice, bs));
+        }
+        HIPCHK(hipEventRecord(p->ev_copy[par], bs));
+        p->copy_rec[par] = true;
+        if (fic_bits) {
+            JF.kind = SRC_FIC;
+            JF.n_cw = 4 * S * F;
+            JF.src = p->ring;
+            JF.src_len = (int64_t)S * p->R * FRAME_SOFT;
+            JF.err = c->err;
+            JF.slots = slots_d;
+            JF.prof = (const Profile *)p->ficprof_d;
+            JF.out = fic_bits;
+            JF.out_stride = 768;
+            JF.prbs = 1;
+            JF.prbs_words = c->prbs;
+            JF.dec = p->dec_d[par] + p->dec_fic_off;
+            JF.dec_ncw = dec_rows(JF.n_cw);
+            JF.dec_nch = dec_chunks(768);
+        }
+        if (do_msc) {
+            JM.kind = SRC_MSC;
+            JM.n_cw = S * 4 * F * p->NSUB;
+            JM.src = p->ring;
+            JM.src_len = (int64_t)S * p->R * FRAME_SOFT;
+            JM.err = c->err;
+            JM.prof = p->prof_d;
+            JM.nsub = p->NSUB;
+            JM.ncif = 4 * F;
+            JM.ring = p->R;
+            JM.cif0s = p->cif0_d + (size_t)par * S;
+            JM.ncifs = p->ncif_d + (size_t)par * S;
+            JM.sub_start = p->substart_d;
+            JM.out = msc_bits;
+            JM.out_stride = msc_stride;
+            JM.prbs = 1;
+            JM.prbs_words = c->prbs;
+            JM.dec = p->dec_d[par];
+            JM.dec_ncw = dec_rows(JM.n_cw);
+            JM.dec_nch = dec_chunks(p->max_nbits);
+        }
+        if (fic_bits && do_msc) {
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
+            HIPCHK(launch_acs_msc_fic(bs, JM, JF));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
+            HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
+        } else if (fic_bits) {
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
+            HIPCHK(launch_viterbi(bs, JF));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
+        } else if (do_msc) {
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
+            HIPCHK(launch_acs(bs, JM));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
+            HIPCHK(launch_traceback(bs, JM));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
+        }
+        return 0;
+    };
+    // Speculative back end: in steady state (every stream synchronised, no coarse AFC
+    // pending) the first front pass commits exactly the frames it predicts, so the
+    // channel decoding of those frames is queued right behind it, before the host has
+    // read and verified the pass -- the GPU does not idle through the host's replay.  If
+    // the replay commits anything else, or a second pass rewrites frames, the back end
+    // is queued again with the committed frames and overwrites the outputs.
+    std::vector<int> pred(S, 0);
+    std::vector<int32_t> pred_slot((size_t)S * F, -1);
+    bool spec = (fic_bits || do_msc) && p->speculate;
+    for (int s = 0; s < S && spec; s++) {
+        const StreamSt &x = cur[s];
+        if (!x.synced || x.f2) { spec = false; break; }
+        int64_t w = x.window;
+        for (int f = 0; f < F; f++) {
+            const int64_t end = w + x.last_si + TU + (int64_t)NSYM * TS;
+            if (end > n_avail[s]) break;
+            pred_slot[(size_t)s * F + f] = (int32_t)((int64_t)s * p->R + (x.frame_count + f) % p->R);
+            pred[s] = f + 1;
+            w = end + TNULL;
+        }
+    }
+    bool spec_sent = false;
+    int passes = 0;
     // ofdmProcessor::run per stream: speculative front-end passes commit frames; a
     // stream that loses sync (or was never synchronised) searches the next null
     // symbol from where it is and continues (goto notSynced, ofdm-processor.cpp:354-357).
@@ -1330,7 +1469,15 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         int found = 0;
         if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) return rc;
         bool progress = false, lost = false;
-        if (int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost)) return rc;
+        std::function<int()> after;
+        if (spec && it == 0 && found == 0)
+            after = [&]() -> int {
+                spec_sent = true;
+                return enqueue_back(pred, pred_slot);
+            };
+        const int64_t launches_before = p->front_launches;
+        if (int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost, after)) return rc;
+        if (p->front_launches != launches_before) passes++;
         if (!progress && !lost && !found) break;
     }
     bool all = true;
@@ -1338,94 +1485,14 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         if (done[s] != F) all = false;
         cur[s].frames_run = done[s];
     }
-    // channel decoding on the pipeline's stream, after this run's front end
-    p->cur = par;
-    hipStream_t bs = p->vs[par];
-    HIPCHK(hipEventRecord(p->ev_front, c->stream));
-    HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
-    // per stream: CIF index of its first CIF slot and the CIFs it delivered
-    {
-        std::vector<int64_t> c0(S);
-        std::vector<int32_t> nc(S);
-        for (int s = 0; s < S; s++) {
-            c0[s] = p->st[s].cif_count;
-            nc[s] = 4 * done[s];
-        }
-        HIPCHK(hipMemcpyAsync(p->cif0_d + (size_t)par * S, c0.data(), sizeof(int64_t) * S, hipMemcpyHostToDevice, bs));
-        HIPCHK(hipMemcpyAsync(p->ncif_d + (size_t)par * S, nc.data(), sizeof(int32_t) * S, hipMemcpyHostToDevice, bs));
-    }
-    // FIC for every committed frame, MSC for all subchannels of every delivered CIF.
-    // With both, one ACS and one traceback launch decode them together (the FIC's short
-    // waves fill the SIMDs the MSC's last waves leave idle); decisions in separate
-    // halves of this stream's decision buffer.
-    VitJob JF, JM;
-    memset(&JF, 0, sizeof JF);
-    memset(&JM, 0, sizeof JM);
-    int32_t *slots_d = p->slots_d + (size_t)par * S * F;
-    if (fic_bits) {
-        std::vector<int32_t> slots((size_t)S * F);
-        for (int s = 0; s < S; s++)
-            for (int f = 0; f < F; f++) slots[(size_t)s * F + f] = f < done[s] ? p->last_frames[(size_t)s * F + f].out_slot : -1;
-        HIPCHK(hipMemcpyAsync(slots_d, slots.data(), sizeof(int32_t) * slots.size(), hipMemcpyHostToDevice, bs));
-        JF.kind = SRC_FIC;
-        JF.n_cw = 4 * S * F;
-        JF.src = p->ring;
-        JF.src_len = (int64_t)S * p->R * FRAME_SOFT;
-        JF.err = c->err;
-        JF.slots = slots_d;
-        JF.prof = (const Profile *)p->ficprof_d;
-        JF.out = fic_bits;
-        JF.out_stride = 768;
-        JF.prbs = 1;
-        JF.prbs_words = c->prbs;
-        JF.dec = p->dec_d[par] + p->dec_fic_off;
-        JF.dec_ncw = dec_rows(JF.n_cw);
-        JF.dec_nch = dec_chunks(768);
-    }
-    if (do_msc) {
-        JM.kind = SRC_MSC;
-        JM.n_cw = S * 4 * F * p->NSUB;
-        JM.src = p->ring;
-        JM.src_len = (int64_t)S * p->R * FRAME_SOFT;
-        JM.err = c->err;
-        JM.prof = p->prof_d;
-        JM.nsub = p->NSUB;
-        JM.ncif = 4 * F;
-        JM.ring = p->R;
-        JM.cif0s = p->cif0_d + (size_t)par * S;
-        JM.ncifs = p->ncif_d + (size_t)par * S;
-        JM.sub_start = p->substart_d;
-        JM.out = msc_bits;
-        JM.out_stride = msc_stride;
-        JM.prbs = 1;
-        JM.prbs_words = c->prbs;
-        JM.dec = p->dec_d[par];
-        JM.dec_ncw = dec_rows(JM.n_cw);
-        JM.dec_nch = dec_chunks(p->max_nbits);
-    }
-    if (fic_bits && do_msc) {
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs_msc_fic(bs, JM, JF));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
-        HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
-    } else if (fic_bits) {
-        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-        HIPCHK(launch_viterbi(bs, JF));
-        if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
-    } else if (do_msc) {
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
-        HIPCHK(launch_acs(bs, JM));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
-        HIPCHK(launch_traceback(bs, JM));
-        HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
-    }
+    std::vector<int32_t> slot((size_t)S * F, -1);
+    for (int s = 0; s < S; s++)
+        for (int f = 0; f < done[s]; f++) slot[(size_t)s * F + f] = p->last_frames[(size_t)s * F + f].out_slot;
+    bool hit = spec_sent && passes == 1 && done == pred && slot == pred_slot;
+    p->spec_runs += spec_sent ? 1 : 0;
+    p->spec_hits += hit ? 1 : 0;
+    if (!hit)
+        if (int rc = enqueue_back(done, slot)) return rc;
     HIPCHK(hipEventRecord(p->ev_back[par], bs));
     p->back_rec[par] = true;
     p->run_idx++;
