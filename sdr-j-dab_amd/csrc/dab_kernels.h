@@ -84,6 +84,7 @@ struct Profile {
     int32_t in_base[5];     // input soft-bit index at segment start / tail start
     uint32_t tail_mask;     // PI_X (24 bits)
     int32_t frag;           // punctured input length (fragment size)
+    int32_t inv_off;        // its inverse table in VitJob::inv (input -> mother position)
 };
 
 enum SrcKind : int32_t {
@@ -118,6 +119,9 @@ struct VitJob {
     int32_t prbs;                   // xor energy-dispersal sequence
     const uint32_t *prbs_words;     // PRBS packed 32 bits per word, bit i = prbs[32w+i]
     const uint8_t *valid;           // optional per-codeword flag: 0 = skip
+    // SRC_MSC / SRC_FIC: inverse depuncturing tables, Profile::frag uint16 mother-code
+    // positions per profile at Profile::inv_off (make_inv); null: step-major loader
+    const uint16_t *inv;
 };
 
 // DAB+ superframe layer (k_dabplus.hip)

@@ -270,6 +270,29 @@ Profile fic_profile() {                      // fic-handler.cpp:254-288
     return p;
 }
 
+// Inverse depuncturing table of a profile: the mother-code position (4 * step + e) of
+// each punctured input, in input order (the same rule as the kernels' idx4 /
+// in_index: PI masks per 128-bit block, then the 24-bit PI_X tail, deconvolve.cpp:172-237)
+std::vector<uint16_t> make_inv(const Profile &P) {
+    std::vector<uint16_t> inv;
+    inv.reserve(P.frag);
+    const int last_end = P.nseg ? P.blk_end[P.nseg - 1] : 0;
+    for (int q = 0; q < 4 * (P.nbits + 6); q++) {
+        const int blk = q >> 7;
+        bool keep;
+        if (blk < last_end) {
+            int k = 0;
+            while (blk >= P.blk_end[k]) k++;
+            keep = (P.mask[k] >> (q & 31)) & 1u;
+        } else {
+            const int b = q - 128 * last_end;
+            keep = b < 24 && ((P.tail_mask >> b) & 1u);
+        }
+        if (keep) inv.push_back((uint16_t)q);
+    }
+    return inv;
+}
+
 }  // namespace
 
 // ----------------------------------------------------------------- context
@@ -284,6 +307,7 @@ struct dabgpu_ctx {
     int16_t *carrier_bin = nullptr;
     float *refarg = nullptr;
     uint8_t *dptab = nullptr;    // DAB+ tables (HostTables::dptab)
+    uint16_t *fic_inv = nullptr; // the FIC profile's inverse depuncturing table (make_inv)
     int32_t *err = nullptr;      // device error word (KERR_* bits)
     int32_t *h_err = nullptr;    // its pinned host copy (read after every synchronising pass)
     OfdmTables T{};
@@ -398,7 +422,8 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->nco, t.nco)) || (rc = upload(c, &c->ref, t.ref)) ||
         (rc = upload(c, &c->w2048, t.w2048)) || (rc = upload(c, &c->carrier_bin, t.carrier_bin)) ||
         (rc = upload(c, &c->prbs, t.prbs_words)) ||
-        (rc = upload(c, &c->refarg, t.refarg)) || (rc = upload(c, &c->dptab, t.dptab))) {
+        (rc = upload(c, &c->refarg, t.refarg)) || (rc = upload(c, &c->dptab, t.dptab)) ||
+        (rc = upload(c, &c->fic_inv, make_inv(fic_profile())))) {
         dabgpu_ctx_destroy(c);
         return rc;
     }
@@ -423,7 +448,7 @@ int dabgpu_ctx_destroy(dabgpu_ctx *c) {
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
     for (void *p : {(void *)c->osc, (void *)c->nco, (void *)c->ref, (void *)c->w2048, (void *)c->carrier_bin, (void *)c->prbs,
-                    (void *)c->refarg, (void *)c->err, (void *)c->dptab})
+                    (void *)c->refarg, (void *)c->err, (void *)c->dptab, (void *)c->fic_inv})
         if (p) (void)hipFree(p);
     if (c->h_err) (void)hipHostFree(c->h_err);
     for (auto p : c->scratch) if (p) (void)hipFree(p);
@@ -657,6 +682,7 @@ int dabgpu_fic_decode_frames(dabgpu_ctx *c, const int16_t *soft, const int32_t *
     J.kind = SRC_FIC;
     J.n_cw = 4 * nf;
     J.src = soft;
+    J.inv = c->fic_inv;
     J.slots = (const int32_t *)sd;
     {
         int32_t mx = 0;
@@ -802,6 +828,7 @@ struct dabgpu_pipe {
     bool back_rec[2] = {false, false};
     int64_t run_idx = 0;
     Profile *ficprof_d = nullptr;
+    uint16_t *inv_d = nullptr;       // the subchannel profiles' inverse depuncturing tables
     // optional per-stage kernel timing (HIP events on the stage's stream)
     int profiling = 0;                          // 1: last run, 2: every run since enabled
     std::vector<hipEvent_t> ev_pool;
@@ -876,6 +903,13 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
         ss[i] = p->sub[i].startAddr * 64;
         p->max_nbits = std::max(p->max_nbits, profs[i].nbits);
     }
+    std::vector<uint16_t> inv;
+    for (int i = 0; i < p->NSUB; i++) {
+        profs[i].inv_off = (int32_t)inv.size();
+        const std::vector<uint16_t> v = make_inv(profs[i]);
+        inv.insert(inv.end(), v.begin(), v.end());
+    }
+    if (inv.empty()) inv.push_back(0);
     const size_t SF = (size_t)p->S * p->F;
     int rc = 0;
     auto A = [&](void **ptr, size_t bytes) {
@@ -910,6 +944,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->dec_d[0], p->dec_sz);
     A((void **)&p->dec_d[1], p->dec_sz);
     A((void **)&p->ficprof_d, sizeof(Profile));
+    A((void **)&p->inv_d, sizeof(uint16_t) * inv.size());
     int prio_least = 0, prio_greatest = 0;
     if (!rc && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) rc = fail(DABGPU_E_HIP, "priority range");
     if (!rc && (hipStreamCreateWithPriority(&p->vs[0], hipStreamNonBlocking, prio_least) != hipSuccess ||
@@ -956,6 +991,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     if (!rc) {
         if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(p->substart_d, ss.data(), sizeof(int32_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(p->inv_d, inv.data(), sizeof(uint16_t) * inv.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemset(p->ring, 0, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
             rc = fail(DABGPU_E_HIP, "pipe init copy failed");
     }
@@ -979,7 +1015,7 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_cif0,
                     (void *)p->h_ncif, (void *)p->h_slots})
         if (h) (void)hipHostFree(h);
-    for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
+    for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->inv_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->cif0_d, (void *)p->ncif_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d})
@@ -1349,8 +1385,6 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     // the MSC's last waves leave idle); decisions in separate halves of the stream's
     // decision buffer.
     auto enqueue_back = [&](const std::vector<int> &dn, const std::vector<int32_t> &slots) -> int {
-        HIPCHK(hipEventRecord(p->ev_front, c->stream));
-        HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
         // per stream: CIF index of its first CIF slot and the CIFs it delivered (the
         // staging half is reused only once its previous uploads have executed)
         if (p->copy_rec[par]) HIPCHK(hipEventSynchronize(p->ev_copy[par]));
@@ -1381,6 +1415,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             JF.err = c->err;
             JF.slots = slots_d;
             JF.prof = (const Profile *)p->ficprof_d;
+            JF.inv = c->fic_inv;
             JF.out = fic_bits;
             JF.out_stride = 768;
             JF.prbs = 1;
@@ -1396,6 +1431,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             JM.src_len = (int64_t)S * p->R * FRAME_SOFT;
             JM.err = c->err;
             JM.prof = p->prof_d;
+            JM.inv = p->inv_d;
             JM.nsub = p->NSUB;
             JM.ncif = 4 * F;
             JM.ring = p->R;
@@ -1410,6 +1446,12 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             JM.dec_ncw = dec_rows(JM.n_cw);
             JM.dec_nch = dec_chunks(p->max_nbits);
         }
+        // the small uploads above run on the back-end stream while the front end still
+        // works; only the decoders wait for it.  (Measured: launching run r's traceback
+        // beside run r+1's ACS instead of beside run r+1's demod is 2 % slower -- the ACS
+        // loses more than the demod gains.)
+        HIPCHK(hipEventRecord(p->ev_front, c->stream));
+        HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
         if (fic_bits && do_msc) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
             HIPCHK(launch_acs_msc_fic(bs, JM, JF));

@@ -428,6 +428,100 @@ template <int NP> struct AcsLds {
     int2 ro2[NP][16];               // SRC_MSC pair: both codewords' row byte offsets per idx & 15
 };
 constexpr int32_t RO_EMPTY = 0x40000000;   // byte offset past any ring: the buffer load returns 0
+// Punctured inputs before mother-code position 4t (t wave-uniform: scalar arithmetic);
+// the same depuncturing rule as idx4 (deconvolve.cpp:172-237, fic-handler.cpp:241-270)
+__device__ __forceinline__ int in_index(const ProfR &P, int t) {
+    const int p = 4 * t, blk = p >> 7;
+    if (blk < P.last_end) {
+        int bs = 0, ib = P.in_base[0];
+        uint32_t m = P.mask[0];
+#pragma unroll
+        for (int k = 1; k < 4; k++) {
+            if (k < P.nseg && blk >= P.blk_end[k - 1]) { bs = P.blk_end[k - 1]; ib = P.in_base[k]; m = P.mask[k]; }
+        }
+        const int n1 = __popc(m);
+        return ib + (blk - bs) * 4 * n1 + ((p & 127) >> 5) * n1 + __popc(m & ((1u << (p & 31)) - 1u));
+    }
+    const int b = p - 128 * P.last_end;
+    return P.tail_base + __popc(b >= 24 ? P.tail_mask : P.tail_mask & ((1u << b) - 1u));
+}
+
+// Input-major tile loader (SRC_MSC / SRC_FIC pairs of one profile).  The tile's steps
+// [t0, t0 + VT) consume the punctured inputs [I0, I1); lane l loads inputs I0 + l + 64k.
+// All of a lane's inputs share the residue (I0 + l) & 15, i.e. one time-interleaver
+// delay-line row per lane and tile, so a soft value costs no address arithmetic (the
+// 64k step is the load's constant offset).  The profile's inverse table (host-built,
+// J.inv + Profile::inv_off: input -> mother-code position) scatters each value pair
+// into an LDS staging table of the tile's 4 * VT mother positions (zero = erasure,
+// deconvolve.cpp:182 / fic-handler.cpp:259), which the branch-metric builder then reads
+// one step per lane.  The step-major loader below spends ~2.4 VALU instructions per
+// trellis step on the depuncturing and delay-line selects of every value; this one 0.9.
+constexpr int IN_K = 4;                    // <= 4 * VT inputs per tile: 4 rounds of 64 lanes
+template <int KIND>
+__device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2], int prof, const ProfR &P, int steps,
+                                             const uint32_t (&row)[6], uint32_t (&x)[1],
+                                             __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2], uint32_t *bm,
+                                             const int2 *ro2, int lane) {
+    const int frag = __builtin_amdgcn_readfirstlane(J.prof[prof].frag);
+    const int ioff = __builtin_amdgcn_readfirstlane(J.prof[prof].inv_off);
+    const __amdgpu_buffer_rsrc_t rinv =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, 2 * frag, 0x00020000);
+    u16x2 vab[IN_K];                       // the pair's inputs, packed
+    uint32_t vm[IN_K];                     // their mother-code positions
+    int I0 = 0, I1 = 0;
+    auto fetch = [&](int t0) {
+        I0 = in_index(P, t0);
+        I1 = in_index(P, min(t0 + VT, steps));
+        const int i = I0 + lane;
+        int2 ro;
+        if constexpr (KIND == SRC_MSC) ro = ro2[i & 15];
+        else ro = make_int2(c[0].valid ? 0 : RO_EMPTY, c[1].valid ? 0 : RO_EMPTY);
+        const int oa = ro.x + 2 * i, ob = ro.y + 2 * i, oi = 2 * i;
+#pragma unroll
+        for (int k = 0; k < IN_K; k++) {
+            if (64 * k < I1 - I0) {
+                vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
+                vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);
+                vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
+            }
+        }
+    };
+    // the staging table (4 * VT words) aliases the bm rows: it is read before they are written
+    auto put = [&](int t0) {
+        if (lane < VT) *(uint4 *)&bm[4 * lane] = make_uint4(0u, 0u, 0u, 0u);
+        wave_sync();
+        const int n = I1 - I0;
+#pragma unroll
+        for (int k = 0; k < IN_K; k++) {
+            if (64 * k < n && lane + 64 * k < n) bm[vm[k] - 4 * t0] = as_u32(vab[k]);
+        }
+        wave_sync();
+        u16x2 sv[4];
+        const uint4 q = *(const uint4 *)&bm[4 * (lane < VT ? lane : 0)];
+        sv[0] = as_pk(q.x);
+        sv[1] = as_pk(q.y);
+        sv[2] = as_pk(q.z);
+        sv[3] = as_pk(q.w);
+        wave_sync();
+        if (lane < VT) put_bm(bm, lane, sv);
+    };
+    const int64_t cstride = 64 * 64;
+    fetch(0);
+    for (int t0 = 0; t0 < steps; t0 += VT) {
+        put(t0);
+        wave_sync();
+        if (t0 + VT < steps) fetch(t0 + VT);
+        for (int u = 0; u < 2; u++) {
+            const int tw = t0 + u * WS;
+            if (tw >= steps) break;
+            const int64_t o = (int64_t)(tw / WS) * cstride;
+            if (tw + WS <= steps) acs_word<1, true>(bm + 2 * WS * u, row, x, WS, drs, rb, o, lane);
+            else acs_word<1, false>(bm + 2 * WS * u, row, x, steps - tw, drs, rb, o, lane);
+        }
+        wave_sync();
+    }
+}
+
 template <int KIND, int NP>
 __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) {
     uint32_t *bm = L.bm;
@@ -488,6 +582,13 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     }
     const int64_t cstride = 64 * 64;                    // words per chunk of a 64-row block
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc((void *)J.dec, (short)0, -1, 0x00020000);
+    if constexpr (KIND == SRC_MSC || KIND == SRC_FIC) {
+        // a pair always shares its profile here: SRC_FIC has one, and an SRC_MSC pair is
+        // two consecutive CIFs of one subchannel (ncif = 4F is even)
+        static_assert(NP == 1, "input-major loader: one codeword pair per wave");
+        acs_tiles_in<KIND>(J, c, c[0].prof, p0, steps, row, x, drs, rb, bm, L.ro2[0], lane);
+    } else {
+    // step-major loader (SRC_MOTHER / SRC_FRAG: a pair may have two profiles)
     // inputs of the next tile are loaded while the current one runs its ACS;
     // lane < VT handles step t0 + lane
     u16x2 s[NP][4];                                      // packed {A, B} soft values, per pair
@@ -571,6 +672,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         }
         wave_sync();
     }
+    }
 }
 
 // Chainback (viterbi.cpp:333-357) from state 0, one lane per codeword.  The 64
@@ -607,8 +709,11 @@ __device__ __forceinline__ void tb_stage(uint32_t *lds, const u32x4 (&r)[TB_LD],
     }
 }
 
+// PRBS words a traceback of nch chunks reads (LDS sized by the launch)
+__host__ __device__ inline int tb_prbs_words(int nch) { return min(TB_PRBS, (nch * WS + WS) / 32 + 2); }
+
 template <int KIND>
-__device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*stage)[TB_WORDS], uint32_t *prbs_l) {
+__device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stage, uint32_t *prbs_l) {
     // a latency-bound chain that issues little: first pick on its SIMD, so it keeps
     // its pace next to throughput-bound waves of other kernels (the next run's demod)
     __builtin_amdgcn_s_setprio(3);
@@ -644,7 +749,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     // the energy-dispersal words in LDS: a vector load of them beside the decision
     // prefetches would wait for every outstanding load (vmcnt(0)) once per chunk
     if (J.prbs) {
-        const int nw = min(TB_PRBS, (tmax + WS) / 32 + 2);
+        const int nw = tb_prbs_words(nch);
         for (int i = lane; i < nw; i += 64) prbs_l[i] = J.prbs_words[i];
         wave_sync();
     }
@@ -760,12 +865,13 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t (*sta
     // ring of three register sets, unrolled so every set is a fixed register range: the
     // wait before staging a set then covers only its own loads, not the two chunks
     // still in flight behind it
+    // one staging buffer: the walk's reads of chunk ch and the staging of ch - 1 are
+    // ordered by the wave_sync that ends the walk (17 KB of LDS per wave, was 37 KB)
     auto chunk = [&](u32x4 (&r)[TB_LD], int ch) {
-        uint32_t *cur = stage[ch & 1];
-        tb_stage(cur, r, lane);
+        tb_stage(stage, r, lane);
         wave_sync();
         ld(r, ch - 3);
-        walk(ch, cur);
+        walk(ch, stage);
     };
     ld(ra, nch - 1);
     ld(rb, nch - 2);
@@ -793,19 +899,19 @@ __global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
     if (b < nwa) acs_body<KA, 1>(A, xcd_order(b, nwa), L);
     else acs_body<KB, 1>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
 }
+// LDS (dynamic): the staging buffer, then tb_prbs_words(dec_nch) PRBS words
 template <int KIND>
 __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
-    __shared__ uint32_t stage[2][TB_WORDS];
-    __shared__ uint32_t prbs_l[TB_PRBS];
-    tb_body<KIND>(J, blockIdx.x, stage, prbs_l);
+    extern __shared__ uint32_t tb_lds[];
+    tb_body<KIND>(J, blockIdx.x, tb_lds, tb_lds + TB_WORDS);
 }
 template <int KA, int KB>
 __global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) {
-    __shared__ uint32_t stage[2][TB_WORDS];
-    __shared__ uint32_t prbs_l[TB_PRBS];
-    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, stage, prbs_l);
-    else tb_body<KB>(B, blockIdx.x - nba, stage, prbs_l);
+    extern __shared__ uint32_t tb_lds[];
+    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, tb_lds, tb_lds + TB_WORDS);
+    else tb_body<KB>(B, blockIdx.x - nba, tb_lds, tb_lds + TB_WORDS);
 }
+static size_t tb_lds_bytes(int nch) { return 4 * (size_t)(TB_WORDS + tb_prbs_words(nch)); }
 
 // FIB CRC check (dab-constants.h:310-340): invert the 16 CRC bits in place, run
 // CRC-CCITT from all-ones over 256 bits, pass iff the register ends at zero.  The CRC is
@@ -840,12 +946,12 @@ __global__ __launch_bounds__(256) void k_fic_post(uint8_t *__restrict__ bits, ui
 }
 
 template <template <int> class K>
-static hipError_t launch_kind(hipStream_t st, const VitJob &job, dim3 grid) {
+static hipError_t launch_kind(hipStream_t st, const VitJob &job, dim3 grid, size_t lds = 0) {
     switch (job.kind) {
-    case SRC_MOTHER: hipLaunchKernelGGL(K<SRC_MOTHER>::fn(), grid, dim3(64), 0, st, job); break;
-    case SRC_FRAG:   hipLaunchKernelGGL(K<SRC_FRAG>::fn(), grid, dim3(64), 0, st, job); break;
-    case SRC_FIC:    hipLaunchKernelGGL(K<SRC_FIC>::fn(), grid, dim3(64), 0, st, job); break;
-    case SRC_MSC:    hipLaunchKernelGGL(K<SRC_MSC>::fn(), grid, dim3(64), 0, st, job); break;
+    case SRC_MOTHER: hipLaunchKernelGGL(K<SRC_MOTHER>::fn(), grid, dim3(64), lds, st, job); break;
+    case SRC_FRAG:   hipLaunchKernelGGL(K<SRC_FRAG>::fn(), grid, dim3(64), lds, st, job); break;
+    case SRC_FIC:    hipLaunchKernelGGL(K<SRC_FIC>::fn(), grid, dim3(64), lds, st, job); break;
+    case SRC_MSC:    hipLaunchKernelGGL(K<SRC_MSC>::fn(), grid, dim3(64), lds, st, job); break;
     default: return hipErrorInvalidValue;
     }
     return hipGetLastError();
@@ -865,7 +971,7 @@ hipError_t launch_acs(hipStream_t st, const VitJob &job) {
 hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
     if (job.dec_ncw < dec_rows(job.n_cw) || job.dec_nch <= 0) return hipErrorInvalidValue;
-    return launch_kind<TbK>(st, job, dim3((job.n_cw + TB_CW - 1) / TB_CW));
+    return launch_kind<TbK>(st, job, dim3((job.n_cw + TB_CW - 1) / TB_CW), tb_lds_bytes(job.dec_nch));
 }
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     hipError_t e = launch_acs(st, job);
@@ -883,7 +989,8 @@ hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) 
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
     const int nba = (a.n_cw + TB_CW - 1) / TB_CW, nbb = (b.n_cw + TB_CW - 1) / TB_CW;
-    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(nba + nbb), dim3(64), 0, st, a, b, nba);
+    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(nba + nbb), dim3(64),
+                       tb_lds_bytes(max(a.dec_nch, b.dec_nch)), st, a, b, nba);
     return hipGetLastError();
 }
 

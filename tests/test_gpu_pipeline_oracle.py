@@ -182,3 +182,40 @@ def test_c5_full_size_superframes_match_reference_path(ctx):
         n, bad, ok3 = n + a, bad + b, ok3 + c
     print("C5 superframe records:", n, "mismatches:", bad, "decoded:", ok3)
     assert bad == 0 and ok3 > 0
+
+
+def _profile_mix():
+    """subchannels covering the depuncturing kinds the pipeline's input-major ACS loader
+    meets (k_viterbi.hip acs_tiles_in): UEP rows with rate-1/4 segments (PI 24: 240
+    inputs per 60-step tile), every UEP level of one bitrate, EEP-A 1-4 incl. the 8 kbit/s
+    special case, EEP-B 1-4 (deconvolve.cpp:39-114,244-314); lengths from the decoder's
+    own fragment sizes, packed into ensembles of <= 864 CUs"""
+    import dabamd
+    kinds = [(384, 1, 1), (192, 1, 1), (32, 1, 1), (80, 1, 1)] + [(96, l, 1) for l in range(1, 6)] + \
+            [(8, 0o101, 0), (8, 0o102, 0), (48, 0o101, 0), (16, 0o102, 0), (24, 0o103, 0), (40, 0o104, 0)] + \
+            [(32, 0o201, 0), (64, 0o202, 0), (96, 0o203, 0), (128, 0o204, 0)]
+    ens, cur, start = [], [], 0
+    for br, prot, uep in kinds:
+        _, frag, _, _ = dabamd.subch_profile(dabamd.Subch(0, 864, br, prot, 0 if uep else 1, 0))
+        n = (frag + 63) // 64
+        if start + n > 864:
+            ens.append(cur)
+            cur, start = [], 0
+        cur.append((start, n, br, prot, uep))
+        start += n
+    ens.append(cur)
+    return ens
+
+
+def test_pipeline_every_profile_kind_matches_reference_path(ctx):
+    """every depuncturing kind through the streaming pipeline at 9 dB (Viterbi decisions
+    that matter): MSC bits of every subchannel and the FIC against the reference path"""
+    F, runs = 4, 5
+    for g, sub in enumerate(_profile_mix()):
+        iqs = _gen(sub, F * runs + 1, [900 + g], 9.0)
+        ref = orc.decode_stream(iqs[0], F * runs, sub)
+        gpu = pc.gpu_decode(ctx, iqs, F, runs, sub)
+        st = pc.compare(gpu[0], ref, sub, check_soft=False)
+        print("profiles", g, [s[2:] for s in sub], st)
+        _check([st], ("profiles", g), soft=False)
+        assert st["msc_cw"] == len(sub) * (4 * F * runs - 16)

@@ -31,6 +31,24 @@ __global__ __launch_bounds__(64) void k_rate(uint32_t *out, int iters) {
                 else if constexpr (OP == 7) asm volatile("v_rcp_f32 %0, %0" : "+v"(v[c]));
                 else if constexpr (OP == 8) asm volatile("v_rndne_f32 %0, %0" : "+v"(v[c]));
                 else if constexpr (OP == 9) asm volatile("v_cvt_i32_f32 %0, %0" : "+v"(v[c]));
+                else if constexpr (OP == 10) asm volatile("v_bfi_b32 %0, %1, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 11) asm volatile("v_lshrrev_b32 %0, 1, %0" : "+v"(v[c]));
+                else if constexpr (OP == 12) asm volatile("v_mov_b32 %0, %1" : "=v"(v[c]) : "v"(v[(c + 1) & 7]));
+                else if constexpr (OP == 13) asm volatile("v_permlane32_swap_b32 %0, %1" : "+v"(v[c]), "+v"(v[(c + 4) & 7]));
+                else if constexpr (OP == 14) asm volatile("s_nop 1\n\tv_add_u32_dpp %0, %0, %1 row_shr:4 row_mask:0xf bank_mask:0xa" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 15) asm volatile("v_pk_sub_i16 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 16) asm volatile("v_alignbit_b32 %0, %0, %1, 31" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 17) asm volatile("v_and_or_b32 %0, %0, %1, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 18) asm volatile("v_lshl_or_b32 %0, %0, 1, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 19) asm volatile("v_cndmask_b32 %0, %0, %1, vcc" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 20) asm volatile("v_xor_b32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 21) asm volatile("v_perm_b32 %0, %0, %1, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 22) asm volatile("v_mul_f32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 23) asm volatile("v_add_u32_e64 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 24) asm volatile("v_sub_u32 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 25) asm volatile("v_lshlrev_b32 %0, 1, %0" : "+v"(v[c]));
+                else if constexpr (OP == 26) asm volatile("v_pk_max_i16 %0, %0, %1" : "+v"(v[c]) : "v"(k1));
+                else if constexpr (OP == 27) asm volatile("v_cmp_gt_u32 vcc, %0, %1" :: "v"(v[c]), "v"(k1) : "vcc");
             }
         }
     }
@@ -109,6 +127,24 @@ int main() {
     run<7>("v_rcp_f32", cus);
     run<8>("v_rndne_f32", cus);
     run<9>("v_cvt_i32_f32", cus);
+    run<10>("v_bfi_b32", cus);
+    run<11>("v_lshrrev_b32", cus);
+    run<12>("v_mov_b32", cus);
+    run<13>("v_permlane32_swap", cus);
+    run<14>("s_nop1+v_add_u32_dpp row_shr", cus);
+    run<15>("v_pk_sub_i16", cus);
+    run<16>("v_alignbit_b32", cus);
+    run<17>("v_and_or_b32", cus);
+    run<18>("v_lshl_or_b32", cus);
+    run<19>("v_cndmask_b32", cus);
+    run<20>("v_xor_b32", cus);
+    run<21>("v_perm_b32", cus);
+    run<22>("v_mul_f32", cus);
+    run<23>("v_add_u32_e64 (VOP3)", cus);
+    run<24>("v_sub_u32", cus);
+    run<25>("v_lshlrev_b32", cus);
+    run<26>("v_pk_max_i16", cus);
+    run<27>("v_cmp_gt_u32", cus);
     run<0, true>("v_pk_add_f32", cus);
     run<1, true>("v_pk_fma_f32", cus);
     run<2, true>("v_pk_mul_f32", cus);
