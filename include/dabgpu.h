@@ -342,8 +342,11 @@ int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op);
 int dabgpu_pipe_sync(dabgpu_pipe *p);
 /* per-stage kernel time (HIP events on each stage's stream, no synchronisation added):
  * dabgpu_pipe_set_profiling(p, 1) times the last dabgpu_pipe_run, (p, 2) every run
- * since the call (summed; launches counts them); 0 turns it off.  set_profiling
- * waits for the pipeline's streams; dabgpu_pipe_timing waits for the recorded work. */
+ * since the call (summed; launches counts them); 0 turns it off.  Mode 3 is mode 2
+ * with every timed stage run alone (the device drained before and after its launch):
+ * per-kernel times without the overlap of the front end and the channel decoders,
+ * for rooflines -- slower, never for throughput.  set_profiling waits for the
+ * pipeline's streams; dabgpu_pipe_timing waits for the recorded work. */
 #define DABGPU_STAGE_PRS      0   /* k_prs_sync   (findIndex)          */
 #define DABGPU_STAGE_BLOCK0   1   /* k_block0     (processBlock_0 AFC) */
 #define DABGPU_STAGE_DEMOD    2   /* k_demod      (processToken x 75)  */

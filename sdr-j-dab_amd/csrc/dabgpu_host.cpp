@@ -830,7 +830,7 @@ struct dabgpu_pipe {
     Profile *ficprof_d = nullptr;
     uint16_t *inv_d = nullptr;       // the subchannel profiles' inverse depuncturing tables
     // optional per-stage kernel timing (HIP events on the stage's stream)
-    int profiling = 0;                          // 1: last run, 2: every run since enabled
+    int profiling = 0;                          // 1: last run, 2: every run since enabled, 3: 2 + stages alone
     std::vector<hipEvent_t> ev_pool;
     std::vector<std::pair<int, int>> ev_rec;   // (stage, index of start event; end = +1)
     float stage_ms[DABGPU_NSTAGE] = {};
@@ -840,6 +840,10 @@ struct dabgpu_pipe {
 static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
     if (!p->profiling) return hipSuccess;
     hipStream_t st = (stage >= DABGPU_STAGE_FIC) ? p->vs[p->cur] : p->c->stream;
+    if (p->profiling == 3) {                    // the stage alone on the device
+        hipError_t r = hipDeviceSynchronize();
+        if (r != hipSuccess) return r;
+    }
     if (start) {
         size_t need = 2 * (p->ev_rec.size() + 1);
         while (p->ev_pool.size() < need) {
@@ -852,7 +856,9 @@ static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
         p->ev_rec.push_back({stage, idx});
         return hipEventRecord(p->ev_pool[idx], st);
     }
-    return hipEventRecord(p->ev_pool[p->ev_rec.back().second + 1], st);
+    hipError_t r = hipEventRecord(p->ev_pool[p->ev_rec.back().second + 1], st);
+    if (r == hipSuccess && p->profiling == 3) r = hipDeviceSynchronize();
+    return r;
 }
 
 namespace {
@@ -1369,7 +1375,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     p->last_si.assign((size_t)S * F, 0);
     p->last_info.assign((size_t)S * F, dabgpu_frame_info());
     p->last_msc = nullptr;
-    if (p->profiling != 2) p->ev_rec.clear();   // mode 2 accumulates over runs
+    if (p->profiling == 1) p->ev_rec.clear();   // modes 2, 3 accumulate over runs
     // at most one run of overlap: run r-2's channel decoding must be done before
     // this run's demod reuses its ring slots
     const int par = (int)(p->run_idx & 1);
@@ -1552,7 +1558,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
 
 int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on) {
     if (!p) return fail(DABGPU_E_ARG, "null pipe");
-    if (on < 0 || on > 2) return fail(DABGPU_E_ARG, "profiling mode %d", on);
+    if (on < 0 || on > 3) return fail(DABGPU_E_ARG, "profiling mode %d", on);
     HIPCHK(hipStreamSynchronize(p->c->stream));         // events of earlier runs are complete
     for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
     p->profiling = on;

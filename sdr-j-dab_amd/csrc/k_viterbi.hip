@@ -33,8 +33,8 @@
 //
 // Decision layout (dab_kernels.h dec_word_index): 64-row blocks, each block's chunks
 // contiguous (a codeword's words then lie within 1.7 MB instead of one per 14 MB stride,
-// which cost the ACS its TLB reach), word [lane] of (row, chunk): bit k = decision of
-// `lane` at trellis step 30*chunk + k (k < 30).
+// which cost the ACS its TLB reach), word [lane] of (row, chunk): bit dpos(k) = decision
+// of `lane` at trellis step 30*chunk + k (k < 30; dpos below).
 #include "dab_device.h"
 #include "dab_kernels.h"
 #include <algorithm>
@@ -299,28 +299,48 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 // (<= 42840 + 1020 < 2^16), so 32-bit adds serve both codewords and the lane moves
 // fold into them as DPP operands: quad_perm for M = 1, 2; for M = 4, 8 the own-lane
 // sum first, then a bank-masked DPP add over the lanes that take their partner's
-// metric; M = 16, 32 go through one permlane swap.  (s_nop 1: the DPP source may have
-// been written by the previous VALU instruction.)
-#define DPP_ADD(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
+// metric; M = 16, 32 go through one permlane swap (a copy, a hazard wait and a
+// quarter-rate swap).  ACS_LDS_MOVES reads P and Q for M = 16, 32 through the LDS
+// crossbar instead (ds_swizzle within 32 lanes, ds_bpermute across the halves; bpa /
+// bpb = byte addresses of lane & 31 and lane | 32): 8 % fewer cycles per step in the
+// ACS alone (tools/acs_core.hip, profiles/r02_acs_core.txt) but no gain in the kernel,
+// whose tile loader also lives on the LDS (profiles/r02_acs_ab.txt): off.
+// DPP hazard: a DPP source written by the previous VALU instruction needs two wait
+// states -- only the first quad_perm add follows the metric update directly (s_nop 1);
+// the bank-masked adds come after the two plain adds that also read x.
+#ifndef ACS_LDS_MOVES
+#define ACS_LDS_MOVES 0            // A/B hook (tools/build_variant.sh): 1 = LDS crossbar
+#endif
+#define DPP_ADD(ctl) "v_add_u32_dpp %0, %1, %2 " ctl
+#define DPP_ADD_NOP(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
 template <int M>
-__device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint32_t &A, uint32_t &B) {
+__device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint32_t &A, uint32_t &B, int bpa,
+                                     int bpb) {
     if constexpr (M == 1) {
-        asm(DPP_ADD("quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
+        asm(DPP_ADD_NOP("quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
         asm(DPP_ADD("quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 2) {
-        asm(DPP_ADD("quad_perm:[0,1,0,1] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
+        asm(DPP_ADD_NOP("quad_perm:[0,1,0,1] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
         asm(DPP_ADD("quad_perm:[2,3,2,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
+    } else if constexpr (M == 16 && ACS_LDS_MOVES) {
+        // swizzle bit mode: lane' = (lane & and) | or within 32 lanes
+        A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x0F) + ta;              // lane & ~16
+        B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 5)) + tb; // lane | 16
+    } else if constexpr (M == 32 && ACS_LDS_MOVES) {
+        A = (uint32_t)__builtin_amdgcn_ds_bpermute(bpa, (int)x) + ta;
+        B = (uint32_t)__builtin_amdgcn_ds_bpermute(bpb, (int)x) + tb;
     } else if constexpr (M == 4) {
         // upper lanes (banks 1,3 of each row) take lane-4 as P; lower lanes (banks 0,2) lane+4 as Q
-        A = x + ta;
-        B = x + tb;
-        asm(DPP_ADD("row_shr:4 row_mask:0xf bank_mask:0xa") : "+v"(A) : "v"(x), "v"(ta));
-        asm(DPP_ADD("row_shl:4 row_mask:0xf bank_mask:0x5") : "+v"(B) : "v"(x), "v"(tb));
+        // (one asm block: the two plain adds are the wait states before the DPP reads x)
+        asm("v_add_u32 %0, %2, %3\n\tv_add_u32 %1, %2, %4\n\t"
+            "v_add_u32_dpp %0, %2, %3 row_shr:4 row_mask:0xf bank_mask:0xa\n\t"
+            "v_add_u32_dpp %1, %2, %4 row_shl:4 row_mask:0xf bank_mask:0x5"
+            : "=&v"(A), "=&v"(B) : "v"(x), "v"(ta), "v"(tb));
     } else if constexpr (M == 8) {
-        A = x + ta;
-        B = x + tb;
-        asm(DPP_ADD("row_shr:8 row_mask:0xf bank_mask:0xc") : "+v"(A) : "v"(x), "v"(ta));
-        asm(DPP_ADD("row_shl:8 row_mask:0xf bank_mask:0x3") : "+v"(B) : "v"(x), "v"(tb));
+        asm("v_add_u32 %0, %2, %3\n\tv_add_u32 %1, %2, %4\n\t"
+            "v_add_u32_dpp %0, %2, %3 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
+            "v_add_u32_dpp %1, %2, %4 row_shl:8 row_mask:0xf bank_mask:0x3"
+            : "=&v"(A), "=&v"(B) : "v"(x), "v"(ta), "v"(tb));
     } else if constexpr (M == 16) {
         auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);   // odd rows <-> even rows
         A = r[0] + ta;
@@ -333,13 +353,26 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
     }
 }
 #undef DPP_ADD
+#undef DPP_ADD_NOP
 
-// w = (w >> 1) with the sign bits of d (bits 15 and 31) inserted at bits 15 and 31:
-// one decision per codeword per step (one v_lshrrev + one v_bfi)
-__device__ __forceinline__ uint32_t dec_in(uint32_t w, uint32_t d) {
+// w = (w >> 1) with the bits of e under mask m inserted (one v_lshrrev + one v_bfi)
+__device__ __forceinline__ uint32_t bits_in(uint32_t m, uint32_t w, uint32_t e) {
     uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(0x80008000u), "v"(d), "v"(w >> 1));
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(e), "v"(w >> 1));
     return r;
+}
+// Decision bits in a stored word.  Per pair of steps (2p, 2p+1) one v_perm joins the
+// bytes holding the four sign bits (bit 7 of {d_2p.b1, d_2p.b3, d_2p+1.b1, d_2p+1.b3})
+// and one v_bfi shifts them into bit 7 of the four bytes of a collector: v_bfi and
+// v_perm issue at half rate on gfx950 (profiles/r02_valu_rate.txt), so 1.5 instead of 2
+// instructions per step.  Collector a takes pairs 0..7, b pairs 8..14; the stored word
+// of codeword 0 is {a.b0, a.b2, b.b0, b.b2}, of codeword 1 {a.b1, a.b3, b.b1, b.b3}.
+// dpos(k) = bit of trellis step k (k < 30) of a chunk in its word.
+#ifndef ACS_DEC_PAIRS
+#define ACS_DEC_PAIRS 1            // A/B hook: 0 = one shift-in per step, dpos(k) = k
+#endif
+__host__ __device__ constexpr int dpos(int k) {
+    return ACS_DEC_PAIRS ? (k < 16 ? 8 * (k & 1) + (k >> 1) : 16 + 8 * (k & 1) + (k >> 1) - 7) : k;
 }
 
 // subtract a common offset from all states of each codeword (see header)
@@ -368,37 +401,56 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (
     const uint32_t *rp[6];
 #pragma unroll
     for (int r = 0; r < 6; r++) rp[r] = bm + row[r];
-    uint32_t w[NP], w0[NP];
+    const int lane = threadIdx.x;
+    const int bpa = 4 * (lane & 31), bpb = 4 * (lane | 32);
+    uint32_t w[NP], w0[NP], dp[NP];
 #pragma unroll
-    for (int p = 0; p < NP; p++) w[p] = 0;
+    for (int p = 0; p < NP; p++) w[p] = dp[p] = 0;
     sfor<0, WS>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         constexpr int rho = j % 6;
+        uint32_t d[NP];
         if (FULL || j < nst) {
             sfor<0, NP>([&](auto pc) {
                 constexpr int p = decltype(pc)::value;
                 const uint2 t = *(const uint2 *)(rp[rho] + p * 8 * BRS + 2 * j);
                 uint32_t A, B;
-                cand<(32 >> rho)>(x[p], t.x, t.y, A, B);
-                w[p] = dec_in(w[p], as_u32(as_pk(B) - as_pk(A)));
+                cand<(32 >> rho)>(x[p], t.x, t.y, A, B, bpa, bpb);
+                d[p] = as_u32(as_pk(B) - as_pk(A));
                 x[p] = as_u32(__builtin_elementwise_min(as_pk(A), as_pk(B)));
             });
         } else {
 #pragma unroll
-            for (int p = 0; p < NP; p++) w[p] = dec_in(w[p], 0u);   // keep the bit positions
+            for (int p = 0; p < NP; p++) d[p] = 0;        // past the codeword: keep the bit positions
         }
-        if constexpr (j == WS / 2 - 1) {
 #pragma unroll
-            for (int p = 0; p < NP; p++) w0[p] = w[p];
+        for (int p = 0; p < NP; p++) {
+            if constexpr (!ACS_DEC_PAIRS) {
+                w[p] = bits_in(0x80008000u, w[p], d[p]);
+            } else if constexpr ((j & 1) == 0) {
+                dp[p] = d[p];
+            } else {
+                w[p] = bits_in(0x80808080u, w[p], __builtin_amdgcn_perm(d[p], dp[p], 0x07050301u));
+            }
+        }
+        if constexpr (j == (ACS_DEC_PAIRS ? 15 : WS / 2 - 1)) {
+#pragma unroll
+            for (int p = 0; p < NP; p++) {
+                w0[p] = w[p];
+                if constexpr (ACS_DEC_PAIRS) w[p] = 0;
+            }
         }
     });
-    // half-word h holds step 15h + k at bit k + 1 (codeword 0) and k + 17 (codeword 1)
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        const uint32_t c0 = ((w0[p] >> 1) & 0x7FFFu) | ((w[p] << 14) & 0x3FFF8000u);
-        const uint32_t c1 = ((w0[p] >> 17) & 0x7FFFu) | ((w[p] >> 2) & 0x3FFF8000u);
-        cw[2 * p] = c0;
-        cw[2 * p + 1] = c1;
+        if constexpr (ACS_DEC_PAIRS) {
+            cw[2 * p] = __builtin_amdgcn_perm(w[p], w0[p], 0x06040200u);
+            cw[2 * p + 1] = __builtin_amdgcn_perm(w[p], w0[p], 0x07050301u);
+        } else {
+            // half-word h holds step 15h + k at bit k + 1 (codeword 0) and k + 17 (codeword 1)
+            cw[2 * p] = ((w0[p] >> 1) & 0x7FFFu) | ((w[p] << 14) & 0x3FFF8000u);
+            cw[2 * p + 1] = ((w0[p] >> 17) & 0x7FFFu) | ((w[p] >> 2) & 0x3FFF8000u);
+        }
     }
 #pragma unroll
     for (int p = 0; p < NP; p++) x[p] = renorm(x[p]);
@@ -809,11 +861,11 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
                 const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);   // phase of step t0+k is k % 6
                 const uint32_t b1 = 1u << p1, b2 = 1u << p2;
                 const uint32_t w1 = mine[lr], c0 = mine[lr & ~b1], c1 = mine[lr | b1];
-                const uint32_t m1 = (uint32_t)((int32_t)(w1 << (31 - k)) >> 31);     // -(bit k)
+                const uint32_t m1 = (uint32_t)((int32_t)(w1 << (31 - dpos(k))) >> 31);     // -(decision k)
                 w |= (k >= p1 ? ((uint32_t)lr << (k - p1)) : ((uint32_t)lr >> (p1 - k))) & (1u << k);
                 lr = (int)((m1 & b1) | ((uint32_t)lr & ~b1));
                 const uint32_t w2 = (m1 & c1) | (~m1 & c0);
-                const uint32_t m2 = (uint32_t)((int32_t)(w2 << (32 - k)) >> 31);
+                const uint32_t m2 = (uint32_t)((int32_t)(w2 << (31 - dpos(k - 1))) >> 31);
                 w |= ((k - 1) >= p2 ? ((uint32_t)lr << (k - 1 - p2)) : ((uint32_t)lr >> (p2 - k + 1))) & (1u << (k - 1));
                 lr = (int)((m2 & b2) | ((uint32_t)lr & ~b2));
             }
@@ -825,7 +877,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
                 const uint32_t w1 = mine[lr];
                 const uint32_t c0 = mine[lr & ~(1 << p1)], c1 = mine[lr | (1 << p1)];
                 {
-                    const int d = (int)((w1 >> k) & 1u);             // predecessor's msb
+                    const int d = (int)((w1 >> dpos(k)) & 1u);       // predecessor's msb
                     const int u = (lr >> p1) & 1;                     // decoded bit of step t0 + k
                     const int nl = (lr & ~(1 << p1)) | (d << p1);
                     if (full || t0 + k < steps) {
@@ -835,7 +887,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
                 }
                 {
                     const uint32_t w2 = ((lr >> p1) & 1) ? c1 : c0;   // = mine[lr]
-                    const int d = (int)((w2 >> (k - 1)) & 1u);
+                    const int d = (int)((w2 >> dpos(k - 1)) & 1u);
                     const int u = (lr >> p2) & 1;
                     const int nl = (lr & ~(1 << p2)) | (d << p2);
                     if (full || t0 + k - 1 < steps) {

@@ -544,7 +544,8 @@ class Pipeline:
         _chk(lib().dabgpu_pipe_sync(self.h), "dabgpu_pipe_sync")
 
     def set_profiling(self, on=True) -> None:
-        """True/1: time the last run; 2: accumulate over every run from now on; False/0: off"""
+        """True/1: time the last run; 2: accumulate over every run from now on; 3: as 2
+        with every stage run alone on the device (roofline timing); False/0: off"""
         mode = 0 if on is False else 1 if on is True else int(on)
         _chk(lib().dabgpu_pipe_set_profiling(self.h, mode), "set_profiling")
 
