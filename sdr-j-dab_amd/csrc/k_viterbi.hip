@@ -361,18 +361,32 @@ __device__ __forceinline__ uint32_t bits_in(uint32_t m, uint32_t w, uint32_t e) 
     asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(e), "v"(w >> 1));
     return r;
 }
-// Decision bits in a stored word.  Per pair of steps (2p, 2p+1) one v_perm joins the
-// bytes holding the four sign bits (bit 7 of {d_2p.b1, d_2p.b3, d_2p+1.b1, d_2p+1.b3})
-// and one v_bfi shifts them into bit 7 of the four bytes of a collector: v_bfi and
-// v_perm issue at half rate on gfx950 (profiles/r02_valu_rate.txt), so 1.5 instead of 2
-// instructions per step.  Collector a takes pairs 0..7, b pairs 8..14; the stored word
-// of codeword 0 is {a.b0, a.b2, b.b0, b.b2}, of codeword 1 {a.b1, a.b3, b.b1, b.b3}.
+// w with the bits of e under mask m (one v_bfi)
+__device__ __forceinline__ uint32_t bits_put(uint32_t m, uint32_t w, uint32_t e) {
+    uint32_t r;
+    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(e), "v"(w));
+    return r;
+}
+// Decision bits in a stored word.  v_bfi and v_perm issue at half rate on gfx950
+// (profiles/r02_valu_rate.txt), the shift at full rate.
+//   ACS_DEC_PAIRS 0: shift-in per step (sign bits 15 / 31 of d), dpos(k) = k.
+//   ACS_DEC_PAIRS 1: per pair of steps (2p, 2p+1) one v_perm joins the bytes holding the
+//     four sign bits (bit 7 of {d_2p.b1, d_2p.b3, d_2p+1.b1, d_2p+1.b3}) and one shift +
+//     v_bfi moves them into bit 7 of the four bytes of a collector.
+//   ACS_DEC_PAIRS 2 (default): the v_perm selectors 8..11 (a byte of copies of bit 15 /
+//     31 of either source) turn the four decisions into four 0x00 / 0xFF bytes at once,
+//     and one v_bfi with the mask 0x01010101 << (p & 7) drops them into bit p & 7 of the
+//     collector's bytes -- no shift: 1 instead of 1.5 instructions per step.
+// Collector a takes pairs 0..7, b pairs 8..14; the stored word of codeword 0 is
+// {a.b0, a.b2, b.b0, b.b2}, of codeword 1 {a.b1, a.b3, b.b1, b.b3}.
 // dpos(k) = bit of trellis step k (k < 30) of a chunk in its word.
 #ifndef ACS_DEC_PAIRS
-#define ACS_DEC_PAIRS 1            // A/B hook: 0 = one shift-in per step, dpos(k) = k
+#define ACS_DEC_PAIRS 2            // A/B hook
 #endif
 __host__ __device__ constexpr int dpos(int k) {
-    return ACS_DEC_PAIRS ? (k < 16 ? 8 * (k & 1) + (k >> 1) : 16 + 8 * (k & 1) + (k >> 1) - 7) : k;
+    return ACS_DEC_PAIRS == 0 ? k
+         : k < 16             ? 8 * (k & 1) + (k >> 1)
+                              : 16 + 8 * (k & 1) + (k >> 1) - (ACS_DEC_PAIRS == 1 ? 7 : 8);
 }
 
 // subtract a common offset from all states of each codeword (see header)
@@ -429,8 +443,10 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (
                 w[p] = bits_in(0x80008000u, w[p], d[p]);
             } else if constexpr ((j & 1) == 0) {
                 dp[p] = d[p];
-            } else {
+            } else if constexpr (ACS_DEC_PAIRS == 1) {
                 w[p] = bits_in(0x80808080u, w[p], __builtin_amdgcn_perm(d[p], dp[p], 0x07050301u));
+            } else {
+                w[p] = bits_put(0x01010101u << ((j >> 1) & 7), w[p], __builtin_amdgcn_perm(d[p], dp[p], 0x0B0A0908u));
             }
         }
         if constexpr (j == (ACS_DEC_PAIRS ? 15 : WS / 2 - 1)) {
