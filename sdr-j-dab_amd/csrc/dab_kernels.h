@@ -145,6 +145,8 @@ struct DpJob {
     int64_t sf_stride;
     dabgpu_superframe *info;        // [S][ncif][ndp]
     const uint8_t *tabs;            // DP_TAB_BYTES: GF exp, log, fire table, alpha^i multiply, CRC
+    int32_t *cand;                  // [S * ndp * ncif] queue of fire-code-passing candidates
+    int32_t *ncand;                 // its length (reset per launch)
 };
 
 hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,

@@ -813,6 +813,7 @@ struct dabgpu_pipe {
     uint8_t *dp_ring_d = nullptr;     // [S][NDP][120*DP_MAX_RS]
     DpState *dp_state_d = nullptr;    // [S][NDP]
     uint8_t *dp_code_d = nullptr;     // [S][NDP][4F] superframe verdict per candidate CIF
+    int32_t *dp_cand_d = nullptr;     // [S*NDP*4F + 1] fire-code-passing candidates + count
     const uint8_t *last_msc = nullptr; // MSC bits of the last run
     int32_t last_msc_stride = 0;
     // channel decoding (FIC/MSC Viterbi, DAB+) of run r runs on back-end stream
@@ -988,6 +989,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
         A((void **)&p->dp_ring_d, (size_t)p->S * p->NDP * 120 * DP_MAX_RS);
         A((void **)&p->dp_state_d, sizeof(DpState) * (size_t)p->S * p->NDP);
         A((void **)&p->dp_code_d, (size_t)p->S * p->NDP * 4 * p->F);
+        A((void **)&p->dp_cand_d, sizeof(int32_t) * ((size_t)p->S * p->NDP * 4 * p->F + 1));
         if (!rc && (hipMemcpy(p->dp_sub_d, dps.data(), sizeof(int32_t) * dps.size(), hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemcpy(p->dp_br_d, dpb.data(), sizeof(int16_t) * dpb.size(), hipMemcpyHostToDevice) != hipSuccess ||
                     hipMemset(p->dp_ring_d, 0, (size_t)p->S * p->NDP * 120 * DP_MAX_RS) != hipSuccess ||
@@ -1024,7 +1026,8 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->inv_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->cif0_d, (void *)p->ncif_d,
-                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d})
+                    (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d,
+                    (void *)p->dp_cand_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
@@ -1612,6 +1615,8 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.ring = p->dp_ring_d;
     J.state = p->dp_state_d;
     J.code = p->dp_code_d;
+    J.ncand = p->dp_cand_d;
+    J.cand = p->dp_cand_d + 1;
     J.sf_out = sf_bytes;
     J.sf_stride = sf_stride;
     J.info = info;

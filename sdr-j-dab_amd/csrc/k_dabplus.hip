@@ -167,12 +167,13 @@ __device__ int rs_solve(const int (&syn)[10], const GfTabs &g, uint8_t *roots, u
 }
 
 // firecode_checker::check (firecode-checker.cpp:76-94) on 11 bytes
-__device__ bool fire_ok(const uint8_t *x, const GfTabs &g) {
-    uint32_t st = ((uint32_t)x[2] << 8) | x[3];
+__device__ __forceinline__ bool fire_ok(const uint32_t (&x)[11], const uint16_t *fire) {
+    uint32_t st = (x[2] << 8) | x[3];
+#pragma unroll
     for (int i = 4; i < 13; i++) {
-        const int b = i < 11 ? x[i] : x[i - 11];          // bytes 4..10 then 0..1
-        const uint32_t is = g.fire[st >> 8];
-        st = ((is & 0xffu) ^ (uint32_t)b) | ((is ^ (st << 8)) & 0xff00u);
+        const uint32_t b = i < 11 ? x[i] : x[i - 11];     // bytes 4..10 then 0..1
+        const uint32_t is = fire[st >> 8];
+        st = ((is & 0xffu) ^ b) | ((is ^ (st << 8)) & 0xff00u);
     }
     return st == 0;
 }
@@ -222,17 +223,47 @@ __device__ __forceinline__ uint32_t wave_xor(uint32_t v) {
     return v;
 }
 
-// Superframe candidates, one wave per (stream, DAB+ subchannel, CIF of the run):
-// the fire code at the oldest block of the 5-CIF window ending at that CIF
-// (firecode-checker.cpp:76-94) and, where it holds, processSuperframe
-// (mp4processor.cpp:146-292): RS(120,110) over the RSDims interleaved columns, AU
-// table, AU CRCs.  Which candidates the reference actually evaluates depends on
-// the superframe state (blocksInBuffer), walked afterwards by k_dp_walk; the
-// verdict of every candidate (0 fire code failed, 2 rejected, 3 decoded) goes to
-// J.code, the record and the corrected bytes of a passing one to their slots.
+// Superframe candidates.  k_dp_fire, one wave per (stream, DAB+ subchannel), one lane
+// per CIF of the run: the fire code at the oldest block of the 5-CIF window ending at
+// that CIF (firecode-checker.cpp:76-94); a window that holds an undelivered CIF or
+// fails is marked 0, a passing one is queued (about one CIF in five once the
+// superframes are aligned).  k_dp_superframe then runs processSuperframe
+// (mp4processor.cpp:146-292) on the queued candidates only -- RS(120,110) over the
+// RSDims interleaved columns, AU table, AU CRCs -- as a grid of resident waves that load
+// the GF tables once and take candidates from the queue (round 1 launched one wave per
+// candidate, each copying the tables, four in five only to fail the fire code).  Which
+// candidates the reference actually evaluates depends on the superframe state
+// (blocksInBuffer), walked afterwards by k_dp_walk; the verdict of every candidate
+// (0 fire code failed, 2 rejected, 3 decoded) goes to J.code, the record and the
+// corrected bytes of a passing one to their slots.
 // The work of one superframe is spread over the wave: syndromes as direct sums
 // (lane = column x a slice of its rows), Berlekamp-Massey/Chien/Forney one column
 // per lane, each AU CRC in 64 slices joined by x^(8d) shifts (the CRC is linear).
+__global__ __launch_bounds__(64) void k_dp_fire(DpJob J) {
+    __shared__ uint16_t fire[256];
+    const int lane = threadIdx.x, sd = blockIdx.x;      // sd = stream * ndp + dp
+    const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
+    const int br = J.dp_br[dp], sub = J.dp_sub[dp], nbytes = 3 * br;
+    const uint16_t *tf = (const uint16_t *)(J.tabs + offsetof(GfTabs, fire));
+    for (int i = lane; i < 256; i += 64) fire[i] = tf[i];
+    wave_sync();
+    const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
+    for (int cl = lane; cl < J.ncif; cl += 64) {
+        uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
+        // a window holding an undelivered CIF (de-interleaver warm-up, or a CIF slot the
+        // stream did not fill in this run) is never evaluated
+        bool ok = !(cl >= J.ncifs[stream] || J.cif0s[stream] + cl - 4 < 16);
+        if (ok) {
+            uint32_t x[11];
+#pragma unroll
+            for (int p = 0; p < 11; p++) x[p] = window_byte(J, carry, stream, sub, nbytes, cl, p);
+            ok = fire_ok(x, fire);
+        }
+        *code = ok ? 1 : 0;
+        if (ok) J.cand[atomicAdd(J.ncand, 1)] = sd * J.ncif + cl;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     __shared__ GfTabs g;
     __shared__ uint8_t sfb[120 * DP_MAX_RS];
@@ -240,142 +271,132 @@ __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     __shared__ uint8_t rl[64 * 40];
     __shared__ int32_t red[64];
     const int lane = threadIdx.x;
-    const int cl = blockIdx.x % J.ncif, sd = blockIdx.x / J.ncif;       // sd = stream * ndp + dp
-    const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
-    const int br = J.dp_br[dp], sub = J.dp_sub[dp];
-    const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
-    uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
-    // a window holding an undelivered CIF (de-interleaver warm-up, or a CIF slot the
-    // stream did not fill in this run) is never evaluated
-    if (cl >= J.ncifs[stream] || J.cif0s[stream] + cl - 4 < 16) {
-        if (lane == 0) *code = 0;
-        return;
-    }
-    const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
     const uint32_t *tabs32 = (const uint32_t *)J.tabs;
-    const int fire0 = offsetof(GfTabs, fire) / 4, fire1 = fire0 + (int)sizeof(g.fire) / 4;
-    for (int i = fire0 + lane; i < fire1; i += 64) ((uint32_t *)&g)[i] = tabs32[i];
-    if (lane < 11) sfb[lane] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, lane);
-    wave_sync();
-    if (!fire_ok(sfb, g)) {
-        if (lane == 0) *code = 0;
-        return;
-    }
-    for (int i = lane; i < (int)sizeof(GfTabs) / 4; i += 64)
-        if (i < fire0 || i >= fire1) ((uint32_t *)&g)[i] = tabs32[i];
-    for (int p = 11 + lane; p < fsz; p += 64) sfb[p] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, p);
-    for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;
-    wave_sync();
-    // syndromes S_i = sum_m r_m alpha^(i (119-m)) per column: the Horner sums of
-    // reed-solomon.cpp:231-266 (roots alpha^0..alpha^9, the 135 zero pad bytes
-    // contribute nothing).  Lane -> column lane % RS, rows lane / RS + k * (64 / RS).
-    const int per = 64 / RS;
-    if (lane < per * RS) {
-        const int j = lane % RS;
-        uint32_t acc[10];
-#pragma unroll
-        for (int i = 0; i < 10; i++) acc[i] = 0;
-        for (int m = lane / RS; m < 120; m += per) {
-            const int r = sfb[j + m * RS];
-            if (r) {
-                const int t = 119 - m;
-                int e = g.log[r];
-                acc[0] ^= g.exp[e];
-#pragma unroll
-                for (int i = 1; i < 10; i++) {
-                    e += t;
-                    if (e >= RS_NN) e -= RS_NN;
-                    acc[i] ^= g.exp[e];
+    for (int i = lane; i < (int)sizeof(GfTabs) / 4; i += 64) ((uint32_t *)&g)[i] = tabs32[i];
+    const int ncand = *J.ncand;                          // k_dp_fire's queue (same stream, before)
+    for (int ci = blockIdx.x; ci < ncand; ci += gridDim.x) {
+        wave_sync();                                         // the previous candidate's LDS reads are done
+        const int id = J.cand[ci];
+        const int cl = id % J.ncif, sd = id / J.ncif;
+        const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
+        const int br = J.dp_br[dp], sub = J.dp_sub[dp];
+        const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
+        uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
+        const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
+        for (int p = lane; p < fsz; p += 64) sfb[p] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, p);
+        for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;
+        wave_sync();
+        // syndromes S_i = sum_m r_m alpha^(i (119-m)) per column: the Horner sums of
+        // reed-solomon.cpp:231-266 (roots alpha^0..alpha^9, the 135 zero pad bytes
+        // contribute nothing).  Lane -> column lane % RS, rows lane / RS + k * (64 / RS).
+        const int per = 64 / RS;
+        if (lane < per * RS) {
+            const int j = lane % RS;
+            uint32_t acc[10];
+    #pragma unroll
+            for (int i = 0; i < 10; i++) acc[i] = 0;
+            for (int m = lane / RS; m < 120; m += per) {
+                const int r = sfb[j + m * RS];
+                if (r) {
+                    const int t = 119 - m;
+                    int e = g.log[r];
+                    acc[0] ^= g.exp[e];
+    #pragma unroll
+                    for (int i = 1; i < 10; i++) {
+                        e += t;
+                        if (e >= RS_NN) e -= RS_NN;
+                        acc[i] ^= g.exp[e];
+                    }
                 }
             }
+    #pragma unroll
+            for (int i = 0; i < 10; i++)
+                if (acc[i]) atomicXor(&syn_s[10 * j + i], acc[i]);
         }
-#pragma unroll
-        for (int i = 0; i < 10; i++)
-            if (acc[i]) atomicXor(&syn_s[10 * j + i], acc[i]);
-    }
-    wave_sync();
-    int ler = 0;
-    if (lane < RS) {                                     // one column per lane
-        int sy[10];
-#pragma unroll
-        for (int i = 0; i < 10; i++) sy[i] = (int)syn_s[10 * lane + i];
-        uint8_t *w = rl + lane * 40;
-        int nf = 0;
-        ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
-        for (int f = 0; f < nf; f++) {
-            const int m = w[20 + f] - RS_PAD;
-            if (m >= 0 && m < 110) sfb[lane + m * RS] ^= w[30 + f];
-        }
-    }
-    red[lane] = ler;
-    wave_sync();
-    // the reference stops at the first failing column
-    int nerr = 0, fail = 0;
-    for (int j = 0; j < RS && !fail; j++) {
-        const int l = red[j];
-        if (l > 0) nerr += l;
-        if (l < 0) fail = 1;
-    }
-    dabgpu_superframe info;
-    info.status = 2;
-    info.num_aus = 0;
-    info.n_corrected = (int16_t)nerr;
-    for (int i = 0; i < 7; i++) info.au_start[i] = 0;
-    info.au_crc_ok = 0;
-    info.reserved = 0;
-    bool ok = !fail;
-    if (ok) {
-        // AU table (:181-233)
-        const int dac = (sfb[2] >> 6) & 1, sbr = (sfb[2] >> 5) & 1;
-        int n, a[7];
-        switch (2 * dac + sbr) {
-        default:
-        case 0: n = 4; a[0] = 8; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
-            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4); a[4] = end; break;
-        case 1: n = 2; a[0] = 5; a[1] = sfb[3] * 16 + (sfb[4] >> 4); a[2] = end; break;
-        case 2: n = 6; a[0] = 11; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
-            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4);
-            a[4] = (sfb[7] & 0xf) * 256 + sfb[8]; a[5] = sfb[9] * 16 + (sfb[10] >> 4); a[6] = end; break;
-        case 3: n = 3; a[0] = 6; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
-            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = end; break;
-        }
-        info.num_aus = (int8_t)n;
-        for (int i = 0; i < 7; i++) info.au_start[i] = (int16_t)(i <= n ? a[i] : 0);
-        int bad = n;                                     // first AU with an impossible layout
-        for (int i = 0; i < n; i++) {
-            const int len = a[i + 1] - a[i] - 2;
-            if (a[i + 1] < a[i] || len >= 960 || len < 0) { bad = i; break; }
-        }
-        // dabPlus_crc (mp4processor.cpp:40-61) of AU i over [a[i], a[i+1]): lane l
-        // runs the table CRC over its slice (lane 0 from the 0xFFFF preset, the others
-        // from 0), shifts it past the bytes after the slice, and the slices XOR
-        // together.  Bytes past the superframe read as zero.
-        uint32_t mask = 0;
-        for (int i = 0; i < bad; i++) {
-            const int ai = a[i], len = a[i + 1] - ai - 2, limit = end - ai;
-            const int cs = (len + 63) >> 6;
-            const int k0 = min(len, lane * cs), k1 = min(len, k0 + cs);
-            uint32_t acc = lane == 0 ? 0xFFFFu : 0u;
-            for (int k = k0; k < k1; k++) {
-                const uint32_t b = k < limit ? sfb[ai + k] : 0u;
-                acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ b) & 0xFFu]) & 0xFFFFu;
+        wave_sync();
+        int ler = 0;
+        if (lane < RS) {                                     // one column per lane
+            int sy[10];
+    #pragma unroll
+            for (int i = 0; i < 10; i++) sy[i] = (int)syn_s[10 * lane + i];
+            uint8_t *w = rl + lane * 40;
+            int nf = 0;
+            ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
+            for (int f = 0; f < nf; f++) {
+                const int m = w[20 + f] - RS_PAD;
+                if (m >= 0 && m < 110) sfb[lane + m * RS] ^= w[30 + f];
             }
-            if (acc) acc = crc_mulmod(acc, g.pow8[len - k1]);
-            acc = wave_xor(acc);
-            const uint32_t hi = len < limit ? sfb[ai + len] : 0u, lo = len + 1 < limit ? sfb[ai + len + 1] : 0u;
-            if (((~((hi << 8) | lo) & 0xFFFFu) ^ acc) == 0) mask |= 1u << i;
         }
-        info.au_crc_ok = (uint8_t)(mask & 0x3F);
-        ok = bad == n;
-    }
-    if (ok) {
-        info.status = 3;
-        uint8_t *o = J.sf_out + (((int64_t)stream * J.ncif + cl) * J.ndp + dp) * J.sf_stride;
-        for (int i = lane; i < end; i += 64) o[i] = sfb[i];
-    }
-    if (lane == 0) {
-        J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
-        *code = (uint8_t)info.status;
+        red[lane] = ler;
+        wave_sync();
+        // the reference stops at the first failing column
+        int nerr = 0, fail = 0;
+        for (int j = 0; j < RS && !fail; j++) {
+            const int l = red[j];
+            if (l > 0) nerr += l;
+            if (l < 0) fail = 1;
+        }
+        dabgpu_superframe info;
+        info.status = 2;
+        info.num_aus = 0;
+        info.n_corrected = (int16_t)nerr;
+        for (int i = 0; i < 7; i++) info.au_start[i] = 0;
+        info.au_crc_ok = 0;
+        info.reserved = 0;
+        bool ok = !fail;
+        if (ok) {
+            // AU table (:181-233)
+            const int dac = (sfb[2] >> 6) & 1, sbr = (sfb[2] >> 5) & 1;
+            int n, a[7];
+            switch (2 * dac + sbr) {
+            default:
+            case 0: n = 4; a[0] = 8; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+                a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4); a[4] = end; break;
+            case 1: n = 2; a[0] = 5; a[1] = sfb[3] * 16 + (sfb[4] >> 4); a[2] = end; break;
+            case 2: n = 6; a[0] = 11; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+                a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4);
+                a[4] = (sfb[7] & 0xf) * 256 + sfb[8]; a[5] = sfb[9] * 16 + (sfb[10] >> 4); a[6] = end; break;
+            case 3: n = 3; a[0] = 6; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+                a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = end; break;
+            }
+            info.num_aus = (int8_t)n;
+            for (int i = 0; i < 7; i++) info.au_start[i] = (int16_t)(i <= n ? a[i] : 0);
+            int bad = n;                                     // first AU with an impossible layout
+            for (int i = 0; i < n; i++) {
+                const int len = a[i + 1] - a[i] - 2;
+                if (a[i + 1] < a[i] || len >= 960 || len < 0) { bad = i; break; }
+            }
+            // dabPlus_crc (mp4processor.cpp:40-61) of AU i over [a[i], a[i+1]): lane l
+            // runs the table CRC over its slice (lane 0 from the 0xFFFF preset, the others
+            // from 0), shifts it past the bytes after the slice, and the slices XOR
+            // together.  Bytes past the superframe read as zero.
+            uint32_t mask = 0;
+            for (int i = 0; i < bad; i++) {
+                const int ai = a[i], len = a[i + 1] - ai - 2, limit = end - ai;
+                const int cs = (len + 63) >> 6;
+                const int k0 = min(len, lane * cs), k1 = min(len, k0 + cs);
+                uint32_t acc = lane == 0 ? 0xFFFFu : 0u;
+                for (int k = k0; k < k1; k++) {
+                    const uint32_t b = k < limit ? sfb[ai + k] : 0u;
+                    acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ b) & 0xFFu]) & 0xFFFFu;
+                }
+                if (acc) acc = crc_mulmod(acc, g.pow8[len - k1]);
+                acc = wave_xor(acc);
+                const uint32_t hi = len < limit ? sfb[ai + len] : 0u, lo = len + 1 < limit ? sfb[ai + len + 1] : 0u;
+                if (((~((hi << 8) | lo) & 0xFFFFu) ^ acc) == 0) mask |= 1u << i;
+            }
+            info.au_crc_ok = (uint8_t)(mask & 0x3F);
+            ok = bad == n;
+        }
+        if (ok) {
+            info.status = 3;
+            uint8_t *o = J.sf_out + (((int64_t)stream * J.ncif + cl) * J.ndp + dp) * J.sf_stride;
+            for (int i = lane; i < end; i += 64) o[i] = sfb[i];
+        }
+        if (lane == 0) {
+            J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
+            *code = (uint8_t)info.status;
+        }
     }
 }
 
@@ -441,7 +462,12 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job) {
     if (job.ndp <= 0 || job.nstreams <= 0) return hipSuccess;
     if (job.ncif < 4) return hipErrorInvalidValue;       // the carry holds the last 4 CIFs
-    hipLaunchKernelGGL(k_dp_superframe, dim3(job.nstreams * job.ndp * job.ncif), dim3(64), 0, st, job);
+    hipError_t e = hipMemsetAsync(job.ncand, 0, sizeof(int32_t), st);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_dp_fire, dim3(job.nstreams * job.ndp), dim3(64), 0, st, job);
+    // resident waves (about 9 per CU at 16.5 KB of LDS each) draining the queue
+    const int nmax = job.nstreams * job.ndp * job.ncif;
+    hipLaunchKernelGGL(k_dp_superframe, dim3(nmax < 256 * 8 ? nmax : 256 * 8), dim3(64), 0, st, job);
     hipLaunchKernelGGL(k_dp_walk, dim3(job.nstreams * job.ndp), dim3(64), 0, st, job);
     return hipGetLastError();
 }
