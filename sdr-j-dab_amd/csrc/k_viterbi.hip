@@ -755,6 +755,11 @@ constexpr int TB_ROW = 65;
 // chunk and register ring for two waves per SIMD: measured slower, 0.41 vs 0.37 ms)
 constexpr int TB_CW = 64;
 constexpr int TB_LD = TB_CW / 4;            // 16-byte loads per lane per chunk
+#ifndef TB_RING
+#define TB_RING 3                          // decision chunks in the register ring (A/B hook: 4 and 5
+                                           // measured no faster, profiles/r02_acs_ab.txt -- the
+                                           // compiler waits vmcnt(0) at each staging anyway)
+#endif
 constexpr int TB_WORDS = TB_CW * TB_ROW;    // one chunk of a wave's codewords
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TB_GROUP = 8;                 // chunks per output flush (240 bits per codeword)
@@ -825,9 +830,10 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
     const uint32_t *blk0 = J.dec + dec_word_index((int64_t)blk * TB_CW, J.dec_nch);
     const int64_t cstride = 64 * 64;
     int lr = 0;                                          // lane index holding the traced state
-    // decision chunks stream in through a 3-deep register ring (2 chunks = 32 KB per
-    // wave in flight while one is walked): the walk itself is short, the loads are not
-    u32x4 ra[TB_LD], rb[TB_LD], rc[TB_LD];
+    // decision chunks stream in through a TB_RING-deep register ring (TB_RING - 1
+    // chunks of 16 KB per wave in flight while one is walked): the walk itself is short,
+    // the loads are not
+    u32x4 rr[TB_RING][TB_LD];
     auto ld = [&](u32x4 (&r)[TB_LD], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
     // Decoded bits leave in groups of TB_GROUP chunks (240 bytes per codeword, 16-byte
     // stores): vector-memory stores pending beside the decision prefetches make the
@@ -930,26 +936,23 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
         }
         wave_sync();
     };
-    // ring of three register sets, unrolled so every set is a fixed register range: the
-    // wait before staging a set then covers only its own loads, not the two chunks
-    // still in flight behind it
+    // the ring's register sets unrolled so every set is a fixed register range: the
+    // wait before staging a set then covers only its own loads, not the chunks still in
+    // flight behind it
     // one staging buffer: the walk's reads of chunk ch and the staging of ch - 1 are
     // ordered by the wave_sync that ends the walk (17 KB of LDS per wave, was 37 KB)
     auto chunk = [&](u32x4 (&r)[TB_LD], int ch) {
         tb_stage(stage, r, lane);
         wave_sync();
-        ld(r, ch - 3);
+        ld(r, ch - TB_RING);
         walk(ch, stage);
     };
-    ld(ra, nch - 1);
-    ld(rb, nch - 2);
-    ld(rc, nch - 3);
-    for (int ch = nch - 1; ch >= 0; ch -= 3) {
-        chunk(ra, ch);
-        if (ch < 1) break;
-        chunk(rb, ch - 1);
-        if (ch < 2) break;
-        chunk(rc, ch - 2);
+    sfor<0, TB_RING>([&](auto ic) { ld(rr[decltype(ic)::value], nch - 1 - decltype(ic)::value); });
+    for (int ch = nch - 1; ch >= 0; ch -= TB_RING) {
+        sfor<0, TB_RING>([&](auto ic) {
+            constexpr int i = decltype(ic)::value;
+            if (ch - i >= 0) chunk(rr[i], ch - i);       // wave-uniform
+        });
     }
 }
 
