@@ -34,10 +34,38 @@ __device__ __forceinline__ int32_t acq_lp(int64_t p, int64_t a, int32_t lpa, int
     return (int32_t)(t < 0 ? t + INPUT_RATE : t);
 }
 
+// The sequential part runs on lane 0 as one tight loop per state.  Per sample the
+// sLevel IIR needs only its own chain (cvt, mul, add, cvt: the 0.00001 * jan_abs term is
+// formed by all lanes beforehand, pj[]), the envelope sum one float add: the value
+// leaving the 50-sample window was inserted at least 43 samples earlier, so a group of 8
+// samples reads its 8 outgoing values before its own insertions.  While searching the
+// dip, a group runs both chains over its 8 samples and then the 8 threshold tests side
+// by side, keeping the states up to the first test that fails (the reference's loop
+// stops there).  The threshold tests
+// (currentStrength / 50 against 0.40 / 0.75 * sLevel, a float division compared in
+// double) take a multiply by 0.02f and fall back to the IEEE division only within 2^-21
+// of the threshold: the quotient and the product differ by less than 2^-22 of it.
+__device__ __forceinline__ bool q50_gt(float cur, double t) {     // fl(cur / 50) > t
+    const double qa = (double)(cur * 0.02f);
+    if (fabs(qa - t) > 0x1p-21 * fabs(qa)) return qa > t;
+    return (double)(cur / 50) > t;
+}
+__device__ __forceinline__ bool q50_lt(float cur, double t) {     // fl(cur / 50) < t
+    const double qa = (double)(cur * 0.02f);
+    if (fabs(qa - t) > 0x1p-21 * fabs(qa)) return qa < t;
+    return (double)(cur / 50) < t;
+}
+__device__ __forceinline__ float slevel_next(float s, double pj) {
+    return (float)(pj + (1 - 0.00001) * (double)s);                // ofdm-processor.cpp:225
+}
+
 __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, const AcqJob *__restrict__ jobs, int n,
                                                 const float2 *__restrict__ osc, AcqResult *__restrict__ res) {
 #pragma clang fp contract(off)
-    __shared__ float ja[ACQ_BLK], hy[ACQ_BLK], env[64];
+    __shared__ __attribute__((aligned(16))) float ja[ACQ_BLK + 8];
+    __shared__ __attribute__((aligned(16))) float hy[ACQ_BLK + 8];
+    __shared__ __attribute__((aligned(16))) double pj[ACQ_BLK + 8];
+    __shared__ float env[64];
     __shared__ int32_t ev[2];                        // lane 0 -> wave: event kind, sample index in block
     const int lane = threadIdx.x;
     if ((int)blockIdx.x >= n) return;
@@ -59,57 +87,137 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
         for (int i = lane; i < nb; i += 64) {
             const int64_t p = pos + i;
             const float2 t = cmul_exact(x[p], osc[acq_lp(p, a, lpa, ph)]);
-            ja[i] = jan_abs(t);
+            const float j = jan_abs(t);
+            ja[i] = j;
             hy[i] = hypotf(t.x, t.y);
+            pj[i] = 0.00001 * (double)j;
         }
         __syncthreads();
         if (lane == 0) {
             int kind = 0, at = nb;                   // 0: block consumed, 1: restart after `at`, 2: found at `at`
-            for (int i = 0; i < nb;) {
-                if (st == WARM || st == INIT) {
-                    sLevel = (float)(0.00001 * (double)ja[i] + (1 - 0.00001) * (double)sLevel);
-                    if (st == INIT) {
-                        env[idx & 63] = ja[i];
-                        cur += env[idx & 63];
-                        idx++;
-                        if (idx == ACQ_INIT) { st = NULLS; counter = 0; }
-                    } else if (++w == ACQ_WARM) {
-                        st = INIT;
-                        idx = 0;
-                        cur = 0.0f;
+            int i = 0;
+            while (i < nb && kind == 0) {
+                if (st == WARM) {                    // 20 T_s samples building sLevel (:280-282)
+                    const int e = min(nb, i + (ACQ_WARM - w));
+                    float sl = sLevel;
+                    int k = i;
+                    for (; k + 8 <= e; k += 8) {
+#pragma unroll
+                        for (int u = 0; u < 8; u++) sl = slevel_next(sl, pj[k + u]);
                     }
-                    i++;
-                    continue;
-                }
-                if (st == NULLS) {
-                    if (cur / 50 > 0.40 * sLevel) {
-                        sLevel = (float)(0.00001 * (double)ja[i] + (1 - 0.00001) * (double)sLevel);
-                        env[idx & 63] = ja[i];
-                        cur += env[idx & 63] - env[(idx - 50) & 63];
-                        idx++;
-                        i++;
-                        if (++counter > TF) {        // hopeless: notSynced
-                            if (jb.scan && attempts > 5) { nosig++; attempts = 0; }
-                            kind = 1; at = i;
-                            break;
-                        }
-                        continue;
-                    }
-                    attempts = 0;
-                    counter = 0;
-                    st = ENDNULL;
-                }
-                if (cur / 50 < 0.75 * sLevel) {
-                    sLevel = (float)(0.00001 * (double)ja[i] + (1 - 0.00001) * (double)sLevel);
-                    env[idx & 63] = hy[i];
-                    cur += env[idx & 63] - env[(idx - 50) & 63];
+                    for (; k < e; k++) sl = slevel_next(sl, pj[k]);
+                    sLevel = sl;
+                    w += e - i;
+                    i = e;
+                    if (w == ACQ_WARM) { st = INIT; idx = 0; cur = 0.0f; }
+                } else if (st == INIT) {             // 50 samples filling the envelope (:286-292)
+                    sLevel = slevel_next(sLevel, pj[i]);
+                    env[idx & 63] = ja[i];
+                    cur += env[idx & 63];
                     idx++;
                     i++;
-                    if (++counter > TNULL + 50) { kind = 1; at = i; break; }
-                    continue;
+                    if (idx == ACQ_INIT) { st = NULLS; counter = 0; }
+                } else if (st == NULLS) {            // SyncOnNull (:299-316)
+                    float sl = sLevel, cs = cur;
+                    int k = i;
+                    bool leave = false;
+                    while (k < nb && !leave) {
+                        // the group's inputs in registers (reads past nb stay inside the arrays)
+                        float old[8], vv[8];
+                        double pp[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            old[u] = env[(idx + u - 50) & 63];
+                            vv[u] = ja[k + u];
+                            pp[u] = pj[k + u];
+                        }
+                        if (k + 8 <= nb && counter + 8 <= TF) {
+                            // a whole group: both chains first, then the 8 threshold tests
+                            // side by side (independent), cut at the first that fails
+                            float sv[9], cv[9];
+                            sv[0] = sl;
+                            cv[0] = cs;
+#pragma unroll
+                            for (int u = 0; u < 8; u++) {
+                                sv[u + 1] = slevel_next(sv[u], pp[u]);
+                                cv[u + 1] = cv[u] + (vv[u] - old[u]);
+                            }
+                            int m = 8;
+#pragma unroll
+                            for (int u = 7; u >= 0; u--)
+                                if (!q50_gt(cv[u], 0.40 * (double)sv[u])) m = u;
+                            sl = sv[8];
+                            cs = cv[8];
+#pragma unroll
+                            for (int u = 7; u >= 0; u--) {
+                                if (m == u) { sl = sv[u]; cs = cv[u]; }
+                                if (u < m) env[(idx + u) & 63] = vv[u];
+                            }
+                            idx += m;
+                            k += m;
+                            counter += m;
+                            leave = m < 8;
+                            continue;
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            if (leave || k >= nb) break;
+                            if (!q50_gt(cs, 0.40 * (double)sl)) { leave = true; break; }
+                            sl = slevel_next(sl, pp[u]);
+                            const float v = vv[u];
+                            env[idx & 63] = v;
+                            cs += v - old[u];
+                            idx++;
+                            k++;
+                            if (++counter > TF) {    // hopeless: notSynced
+                                if (jb.scan && attempts > 5) { nosig++; attempts = 0; }
+                                kind = 1; at = k;
+                                leave = true;
+                            }
+                        }
+                    }
+                    sLevel = sl;
+                    cur = cs;
+                    i = k;
+                    if (kind == 0 && k < nb) {       // the dip: SyncOnEndNull (:317-319)
+                        attempts = 0;
+                        counter = 0;
+                        st = ENDNULL;
+                    }
+                } else {                             // SyncOnEndNull (:322-337)
+                    float sl = sLevel, cs = cur;
+                    int k = i;
+                    bool leave = false;
+                    while (k < nb && !leave) {
+                        float old[8], vv[8];
+                        double pp[8];
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            old[u] = env[(idx + u - 50) & 63];
+                            vv[u] = hy[k + u];
+                            pp[u] = pj[k + u];
+                        }
+#pragma unroll
+                        for (int u = 0; u < 8; u++) {
+                            if (leave || k >= nb) break;
+                            if (!q50_lt(cs, 0.75 * (double)sl)) {
+                                kind = 2; at = k;    // end of the null symbol: SyncOnPhase at sample k
+                                leave = true;
+                                break;
+                            }
+                            sl = slevel_next(sl, pp[u]);
+                            const float v = vv[u];
+                            env[idx & 63] = v;
+                            cs += v - old[u];
+                            idx++;
+                            k++;
+                            if (++counter > TNULL + 50) { kind = 1; at = k; leave = true; }
+                        }
+                    }
+                    sLevel = sl;
+                    cur = cs;
+                    i = k;
                 }
-                kind = 2; at = i;                    // end of the null symbol: SyncOnPhase at sample `at`
-                break;
             }
             ev[0] = kind;
             ev[1] = at;
