@@ -1183,18 +1183,25 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         const int kChunks = demod_chunks(n, 2);
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
-        HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n, p->fc_d));
-        HIPCHK(hipMemcpyAsync(p->h_fc, p->fc_d, sizeof(float2) * n, hipMemcpyDeviceToHost, c->stream));
-        HIPCHK(hipMemcpyAsync(p->h_snr, p->snr_d, sizeof(int16_t) * n, hipMemcpyDeviceToHost, c->stream));
+        // the host's values and the error word straight into pinned memory (no copies)
+        HIPCHK(launch_front_publish(c->stream, p->fcpart_d, kChunks, n, (float *)p->fc_d, (float *)p->h_fc, p->si_d,
+                                    p->h_si, p->snr_d, p->h_snr, c->err, c->h_err));
     } else {
         HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
         HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
         HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
+        HIPCHK(hipMemcpyAsync(p->h_si, p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     }
-    HIPCHK(hipMemcpyAsync(p->h_si, p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     if (after_launch)
         if (int rc = after_launch()) return rc;
-    if (int rc = kernel_errors(c)) return rc;
+    if (fast) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        if (const int32_t e = *(volatile int32_t *)c->h_err)
+            return fail(DABGPU_E_BOUNDS, "kernel refused out-of-bounds work:%s%s", (e & KERR_FRAME) ? " frame descriptor" : "",
+                        (e & KERR_VITERBI) ? " viterbi source" : "");
+    } else if (int rc = kernel_errors(c)) {
+        return rc;
+    }
     memcpy(si.data(), p->h_si, sizeof(int32_t) * n);
     if (fast) {
         memcpy(fc_all.data(), p->h_fc, sizeof(float2) * n);

@@ -272,7 +272,33 @@ __global__ void k_fc_reduce(const float2 *__restrict__ part, int nchunks, int n,
     out[f] = a;
 }
 
+// k_fc_reduce for the pipeline's front pass, publishing what the host replay reads
+// straight into its pinned buffers (startIndex, FreqCorr, SNR per frame, and the
+// device error word, taken and cleared): the four small read-back copies were blit
+// kernels queued between the demod and the next ACS (~45 us per step).
+__global__ void k_front_publish(const float2 *__restrict__ part, int nchunks, int n, float2 *__restrict__ fc_d,
+                                float2 *h_fc, const int32_t *__restrict__ si_d, int32_t *h_si,
+                                const int16_t *__restrict__ snr_d, int16_t *h_snr, int32_t *err, int32_t *h_err) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f == 0) *h_err = atomicExch(err, 0);
+    if (f >= n) return;
+    float2 a = make_float2(0.0f, 0.0f);
+    for (int c = 0; c < nchunks; c++) { a.x += part[f * nchunks + c].x; a.y += part[f * nchunks + c].y; }
+    fc_d[f] = a;
+    h_fc[f] = a;
+    h_si[f] = si_d[f];
+    h_snr[f] = snr_d[f];
+}
+
 // ---- launchers -----------------------------------------------------------
+hipError_t launch_front_publish(hipStream_t st, const float *part, int nchunks, int n, float *fc_d, float *h_fc,
+                                const int32_t *si_d, int32_t *h_si, const int16_t *snr_d, int16_t *h_snr,
+                                int32_t *err, int32_t *h_err) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_front_publish, dim3((n + 63) / 64), dim3(64), 0, st, (const float2 *)part, nchunks, n,
+                       (float2 *)fc_d, (float2 *)h_fc, si_d, h_si, snr_d, h_snr, err, h_err);
+    return hipGetLastError();
+}
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_fc_reduce, dim3((n + 63) / 64), dim3(64), 0, st, (const float2 *)part, nchunks, n, (float2 *)out);
