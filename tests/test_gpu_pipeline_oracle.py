@@ -219,3 +219,52 @@ def test_pipeline_every_profile_kind_matches_reference_path(ctx):
         print("profiles", g, [s[2:] for s in sub], st)
         _check([st], ("profiles", g), soft=False)
         assert st["msc_cw"] == len(sub) * (4 * F * runs - 16)
+
+
+def test_pipeline_solo_profiling_leaves_outputs_unchanged(ctx):
+    """profiling mode 3 (every stage alone on the device, bench.py's solo steps) times the
+    stages without changing what the pipeline decodes: FIC bits + CRCs, MSC bits and DAB+
+    superframe records of the same IQ with profiling off and in mode 3 are identical, and
+    every stage that ran has a positive time"""
+    import dabamd
+    sub = [(0, 96, 128, 3, 1), (96, 48, 64, 0o103, 0, 1), (144, 48, 64, 0o103, 0, 1)]
+    F, runs = 3, 4
+    iqs = _gen(sub, F * runs + 1, [61, 62], 20.0)
+    S = len(iqs)
+    stride = max(len(x) // 2 for x in iqs)
+    buf = np.zeros((S, 2 * stride), np.float32)
+    for s, x in enumerate(iqs):
+        buf[s, :len(x)] = x
+    diq = ctx.put(buf)
+    subs = [dabamd.Subch(sc[0], sc[1], sc[2], sc[3], 0 if sc[4] else 1,
+                         dabamd.SUBCH_DABPLUS if (len(sc) > 5 and sc[5]) else 0) for sc in sub]
+    outs = []
+    try:
+        for mode in (0, 3):
+            pipe = dabamd.Pipeline(ctx, S, F, subs)
+            try:
+                pipe.set_profiling(mode)
+                got = []
+                for r in range(runs):
+                    fic, crc, msc, valid = pipe.run(diq, stride, [stride] * S, download=True)
+                    info, sfb = pipe.dabplus(download=True)
+                    got.append((fic.copy(), crc.copy(), msc.copy(), valid.copy(), info.copy(), sfb.copy()))
+                pipe.sync()
+                if mode == 3:
+                    t = pipe.timing()
+                    for k in ("demod", "msc_acs", "msc_traceback", "dabplus"):
+                        assert t[k][1] > 0 and t[k][0] > 0.0, (k, t)
+                outs.append(got)
+            finally:
+                pipe.close()
+    finally:
+        diq.free()
+    for r in range(runs):
+        (fa, ca, ma, va, ia, sa), (fb, cb, mb, vb, ib, sb) = outs[0][r], outs[1][r]
+        assert np.array_equal(fa, fb) and np.array_equal(ca, cb) and np.array_equal(va, vb), r
+        v = va.astype(bool)                 # CIF slots a run did not deliver hold old contents
+        assert np.array_equal(ma[v], mb[v]), r
+        assert np.array_equal(ia, ib), r
+        d = ia["status"] == 3
+        assert np.array_equal(sa[d], sb[d]), r
+    assert outs[0][-1][3].any() and (outs[0][-1][4]["status"] == 3).any()
