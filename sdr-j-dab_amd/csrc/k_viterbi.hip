@@ -834,7 +834,13 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
     // chunks of 16 KB per wave in flight while one is walked): the walk itself is short,
     // the loads are not
     u32x4 rr[TB_RING][TB_LD];
+#ifdef TB_AB_NOLOAD          // A/B timing only: chunks after the ring's first fill re-walk stale words
+    auto ld = [&](u32x4 (&r)[TB_LD], int ch) {
+        if (ch >= nch - TB_RING) tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane);
+    };
+#else
     auto ld = [&](u32x4 (&r)[TB_LD], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
+#endif
     // Decoded bits leave in groups of TB_GROUP chunks (240 bytes per codeword, 16-byte
     // stores): vector-memory stores pending beside the decision prefetches make the
     // compiler wait for every outstanding load (vmcnt(0)), so they come rarely.
