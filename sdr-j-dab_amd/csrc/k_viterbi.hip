@@ -299,17 +299,19 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 // (<= 42840 + 1020 < 2^16), so 32-bit adds serve both codewords and the lane moves
 // fold into them as DPP operands: quad_perm for M = 1, 2; for M = 4, 8 the own-lane
 // sum first, then a bank-masked DPP add over the lanes that take their partner's
-// metric; M = 16, 32 go through one permlane swap (a copy, a hazard wait and a
-// quarter-rate swap).  ACS_LDS_MOVES reads P and Q for M = 16, 32 through the LDS
-// crossbar instead (ds_swizzle within 32 lanes, ds_bpermute across the halves; bpa /
-// bpb = byte addresses of lane & 31 and lane | 32): 8 % fewer cycles per step in the
-// ACS alone (tools/acs_core.hip, profiles/r02_acs_core.txt) but no gain in the kernel,
-// whose tile loader also lives on the LDS (profiles/r02_acs_ab.txt): off.
+// metric; M = 32 goes through one permlane swap (a copy, a hazard wait and a
+// quarter-rate swap), M = 16 reads P and Q through the LDS crossbar (two ds_swizzle
+// within 32 lanes), which leaves that step's VALU to the two adds.  ACS_LDS_MOVES 2 also
+// moves M = 32 to the crossbar (ds_bpermute across the halves; bpa / bpb = byte
+// addresses of lane & 31 and lane | 32): 8 % fewer cycles per step in the ACS alone
+// (tools/acs_core.hip, profiles/r02_acs_core.txt) but slower in the kernel, whose tile
+// loader also lives on the LDS; M = 16 alone measured 1.5 % faster (r02_acs_ab.txt).
 // DPP hazard: a DPP source written by the previous VALU instruction needs two wait
 // states -- only the first quad_perm add follows the metric update directly (s_nop 1);
 // the bank-masked adds come after the two plain adds that also read x.
 #ifndef ACS_LDS_MOVES
-#define ACS_LDS_MOVES 0            // A/B hook (tools/build_variant.sh): 1 = LDS crossbar
+#define ACS_LDS_MOVES 1            // A/B hook (tools/build_variant.sh): 0 = permlane swaps only,
+                                   // 1 = M = 16 through the LDS crossbar, 2 = M = 16 and 32
 #endif
 #define DPP_ADD(ctl) "v_add_u32_dpp %0, %1, %2 " ctl
 #define DPP_ADD_NOP(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
@@ -326,7 +328,7 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
         // swizzle bit mode: lane' = (lane & and) | or within 32 lanes
         A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x0F) + ta;              // lane & ~16
         B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 5)) + tb; // lane | 16
-    } else if constexpr (M == 32 && ACS_LDS_MOVES) {
+    } else if constexpr (M == 32 && ACS_LDS_MOVES >= 2) {
         A = (uint32_t)__builtin_amdgcn_ds_bpermute(bpa, (int)x) + ta;
         B = (uint32_t)__builtin_amdgcn_ds_bpermute(bpb, (int)x) + tb;
     } else if constexpr (M == 4) {
