@@ -301,7 +301,7 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 // sum first, then a bank-masked DPP add over the lanes that take their partner's
 // metric; M = 32 goes through one permlane swap (a copy, a hazard wait and a
 // quarter-rate swap), M = 16 reads P and Q through the LDS crossbar (two ds_swizzle
-// within 32 lanes), which leaves that step's VALU to the two adds.  ACS_LDS_MOVES 2 also
+// within 32 lanes), which leaves that step's VALU to the two adds.  ACS_LDS_MOVES bit 1
 // moves M = 32 to the crossbar (ds_bpermute across the halves; bpa / bpb = byte
 // addresses of lane & 31 and lane | 32): 8 % fewer cycles per step in the ACS alone
 // (tools/acs_core.hip, profiles/r02_acs_core.txt) but slower in the kernel, whose tile
@@ -310,8 +310,8 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 // states -- only the first quad_perm add follows the metric update directly (s_nop 1);
 // the bank-masked adds come after the two plain adds that also read x.
 #ifndef ACS_LDS_MOVES
-#define ACS_LDS_MOVES 1            // A/B hook (tools/build_variant.sh): 0 = permlane swaps only,
-                                   // 1 = M = 16 through the LDS crossbar, 2 = M = 16 and 32
+#define ACS_LDS_MOVES 1            // A/B hook (tools/build_variant.sh): bit 0 = M = 16 through
+                                   // the LDS crossbar, bit 1 = M = 32; 0 = permlane swaps only
 #endif
 #define DPP_ADD(ctl) "v_add_u32_dpp %0, %1, %2 " ctl
 #define DPP_ADD_NOP(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
@@ -324,11 +324,11 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
     } else if constexpr (M == 2) {
         asm(DPP_ADD_NOP("quad_perm:[0,1,0,1] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
         asm(DPP_ADD("quad_perm:[2,3,2,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
-    } else if constexpr (M == 16 && ACS_LDS_MOVES) {
+    } else if constexpr (M == 16 && (ACS_LDS_MOVES & 1)) {
         // swizzle bit mode: lane' = (lane & and) | or within 32 lanes
         A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x0F) + ta;              // lane & ~16
         B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 5)) + tb; // lane | 16
-    } else if constexpr (M == 32 && ACS_LDS_MOVES >= 2) {
+    } else if constexpr (M == 32 && (ACS_LDS_MOVES & 2)) {
         A = (uint32_t)__builtin_amdgcn_ds_bpermute(bpa, (int)x) + ta;
         B = (uint32_t)__builtin_amdgcn_ds_bpermute(bpb, (int)x) + tb;
     } else if constexpr (M == 4) {
