@@ -311,7 +311,7 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 // the bank-masked adds come after the two plain adds that also read x.
 #ifndef ACS_LDS_MOVES
 #define ACS_LDS_MOVES 1            // A/B hook (tools/build_variant.sh): bit 0 = M = 16 through
-                                   // the LDS crossbar, bit 1 = M = 32; 0 = permlane swaps only
+                                   // the LDS crossbar, bit 1 = M = 32, bit 2 = M = 8, bit 3 = M = 4
 #endif
 #define DPP_ADD(ctl) "v_add_u32_dpp %0, %1, %2 " ctl
 #define DPP_ADD_NOP(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
@@ -331,6 +331,10 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
     } else if constexpr (M == 32 && (ACS_LDS_MOVES & 2)) {
         A = (uint32_t)__builtin_amdgcn_ds_bpermute(bpa, (int)x) + ta;
         B = (uint32_t)__builtin_amdgcn_ds_bpermute(bpb, (int)x) + tb;
+    } else if constexpr ((M == 4 && (ACS_LDS_MOVES & 8)) || (M == 8 && (ACS_LDS_MOVES & 4))) {
+        // swizzle bit mode: P = lane & ~M, Q = lane | M
+        A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F & ~M) + ta;
+        B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 5)) + tb;
     } else if constexpr (M == 4) {
         // upper lanes (banks 1,3 of each row) take lane-4 as P; lower lanes (banks 0,2) lane+4 as Q
         // (one asm block: the two plain adds are the wait states before the DPP reads x)
