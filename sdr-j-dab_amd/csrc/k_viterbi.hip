@@ -539,7 +539,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
     const int frag = __builtin_amdgcn_readfirstlane(J.prof[prof].frag);
     const int ioff = __builtin_amdgcn_readfirstlane(J.prof[prof].inv_off);
     const __amdgpu_buffer_rsrc_t rinv =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, 2 * frag, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, (ACS_INV_PAIRS ? 4 : 2) * frag, 0x00020000);
     u16x2 vab[IN_K];                       // the pair's inputs, packed
     uint32_t vm[IN_K];                     // their mother-code positions
     int I0 = 0, I1 = 0;
@@ -550,13 +550,19 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         int2 ro;
         if constexpr (KIND == SRC_MSC) ro = ro2[i & 15];
         else ro = make_int2(c[0].valid ? 0 : RO_EMPTY, c[1].valid ? 0 : RO_EMPTY);
-        const int oa = ro.x + 2 * i, ob = ro.y + 2 * i, oi = 2 * i;
+        const int oa = ro.x + 2 * i, ob = ro.y + 2 * i, oi = (ACS_INV_PAIRS ? 4 : 2) * i;
 #pragma unroll
         for (int k = 0; k < IN_K; k++) {
             if (64 * k < I1 - I0) {
                 vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
                 vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);
-                vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
+                if constexpr (!ACS_INV_PAIRS) {
+                    vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
+                } else if ((k & 1) == 0) {                // rounds k, k + 1 (unrolled: k constant)
+                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rinv, oi, 512 * (k >> 1), 0);   // entry i + 128 * (k / 2)
+                    vm[k] = v & 0xFFFFu;
+                    if (k + 1 < IN_K) vm[k + 1] = v >> 16;
+                }
             }
         }
     };
