@@ -10,16 +10,23 @@ acquired (null search) during warm-up.  --cfo HZ runs the same workload through 
 carrier frequency offset (the general NCO path: per-sample oscillator indices,
 running coarse/fine AFC).
 
+Synthetic streams are cyclic (dabsynth_generate_period): each ensemble is one period
+of P = 2F frames (5F with DAB+) repeated end to end -- the time interleaver and the
+superframe grid wrap around the period, so the stream is valid across the seams and
+the decoder does the same work everywhere; synthesis costs P frames per ensemble
+instead of the whole run's.
+
 Multi-GPU (C4): one process per GPU.  `python bench.py --gpus N` starts the N ranks
 itself (torch.distributed.run, 127.0.0.1) unless it already runs under a launcher.
 --iq-source local (default): each rank generates its own ensembles (seeded by rank)
 straight into its HBM -- no data-path collective, weak scaling.  --iq-source rccl:
-rank 0 holds every rank's IQ as int16 (.sdr samples) and scatters each step's chunk
-to the ranks with grouped send/recv over RCCL (xGMI) while they decode the previous
-one; the receivers convert the samples to cf32 on the GPU (dabgpu_iq_convert).  With
-N > 1 the default run also measures that scatter on its own ("stream_split"), so the
-link-bound rate is reported beside the rank-local one.  value = symbols decoded by
-all ranks / max-over-ranks time.
+rank 0 holds every rank's (distinct) ensembles as int16 .sdr samples and sends each
+rank chunk k of ITS streams per step with grouped send/recv over RCCL (xGMI) while the
+ranks decode the previous chunk (StreamSplit); the receivers convert the samples to
+cf32 on the GPU (dabgpu_iq_convert).  With N > 1 the default run also measures that
+transfer on its own ("stream_split"), so the link-bound rate is reported beside the
+rank-local one.  Every rank checks one step of its ensemble 0 against the transmitted
+bits.  value = symbols decoded by all ranks / max-over-ranks time.
 """
 import argparse
 import json
@@ -128,6 +135,97 @@ def chunk_layout(stream_len, F):
     """samples per stream chunk (F frames) and the number of chunks covering a stream"""
     cs = F * TF
     return cs, (stream_len + cs - 1) // cs
+
+
+def period_frames(F, dabplus):
+    """Frames of the cyclic period every synthetic stream repeats (dabsynth_generate_period):
+    a multiple of the step's F frames (the stream split then ships P / F distinct chunk
+    phases) whose 4P CIFs hold whole DAB+ superframes (5 CIFs)."""
+    m = 2
+    while dabplus and (4 * F * m) % 5:
+        m += 1
+    return F * m
+
+
+def chunk_phases(ens, P, cs, E, seed0, threads):
+    """int16 IQ (.sdr samples) of E cyclic streams (seeds seed0 + e) as the P * TF / cs
+    distinct stream chunks: [phase j][ensemble][2 * cs] = stream samples [j cs, (j+1) cs),
+    which chunk k = j + i P/F repeats."""
+    m = P * TF // cs
+    out = np.zeros((m, E, 2 * cs), np.int16)
+    for g0 in range(0, E, 8):
+        n = min(8, E - g0)
+        per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
+        for j in range(m):
+            for p, q, c in ens.stream_pieces(P, j * cs, cs):
+                o = p - j * cs
+                out[j, g0:g0 + n, 2 * o:2 * (o + c)] = to_s16(per[:, 2 * q:2 * (q + c)])
+        del per
+    return out
+
+
+class StreamSplit:
+    """The C4 stream split (BASELINE configs[3]): rank 0 holds every rank's
+    streams and, per step, sends rank r (r >= 1) chunk k of rank r's own ensembles in one
+    grouped send/recv (ncclGroupStart/End under RCCL over xGMI).  src (rank 0): per
+    destination rank an int16 tensor [phases][E][2 * cs] (chunk_phases); chunk k is phase
+    k % phases.  begin(k) starts moving chunk k; end(k, reqs) waits and returns this
+    rank's [E][2 * cs] chunk (None past the last chunk)."""
+
+    def __init__(self, dist, rank, world, E, cs, phases, nchunks, device, src=None):
+        import torch
+        self.dist, self.rank, self.world, self.phases, self.nchunks = dist, rank, world, phases, nchunks
+        self.src = src
+        self.recv = torch.zeros((E, 2 * cs), dtype=torch.int16, device=device) if rank else None
+
+    def begin(self, k):
+        if k >= self.nchunks:
+            return None
+        sends = [s[k % self.phases] for s in self.src] if self.rank == 0 else None
+        return scatter_chunk(self.dist, self.rank, self.world, sends, self.recv)
+
+    def end(self, k, reqs):
+        if k >= self.nchunks:
+            return None
+        for r in reqs or []:
+            r.wait()
+        if self.rank == 0:
+            return self.src[0][k % self.phases]
+        if self.recv.is_cuda:
+            import torch
+            torch.cuda.current_stream().synchronize()
+        return self.recv
+
+
+def check_step(truth, P, st0, st1, fic, crc, msc, valid, subch):
+    """The checked step of ensemble 0: decoded FIC blocks (CRC field restored) and MSC
+    codewords against the transmitted bits of its cyclic stream (frame f of the stream
+    is frame f mod P of the period, receiver CIF n carries CIF n mod 4P's truth)."""
+    f0 = st1.frames_run
+    cif0 = st0.cif_count
+    flip = _crc_flip()
+    fic_ok = all(np.array_equal(fic[0, f, b] ^ flip, truth["fic"][(cif0 // 4 + f) % P, b])
+                 for f in range(f0) for b in range(4))
+    msc_ok = msc_n = 0
+    for c in range(4 * f0):
+        if not valid[0, c]:
+            continue
+        for k, sc in enumerate(subch):
+            nb = 24 * sc[2]
+            msc_n += 1
+            msc_ok += int(np.array_equal(msc[0, c, k, :nb], truth["msc"][(cif0 + c) % (4 * P), k, :nb]))
+    return {"ensemble": 0, "frames": int(f0), "fic_blocks_equal_transmitted": bool(fic_ok),
+            "fic_crc_pass_rate": float(crc[0, :f0].mean()) if f0 else 0.0, "msc_codewords": msc_n,
+            "msc_equal_transmitted": msc_ok}
+
+
+def gather_objects(dist, obj):
+    """obj of every rank, in rank order (a one-element list for one rank)"""
+    if dist is None:
+        return [obj]
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
 
 
 def scatter_chunk(dist, rank, world, sends, recv):
@@ -340,84 +438,61 @@ def main():
     # +1 step: the checked pass; then the solo steps
     total_frames = F * (args.warmup + args.steps + 1 + args.solo_steps) + 1
     ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0, cfo_hz=args.cfo)
+    P = period_frames(F, dabplus)
     ctx = dabamd.Context(rank_device(local))
     stride = ens.length
     rccl = args.iq_source == "rccl" and world > 1
-    # IQ generated in groups straight into HBM: host memory stays at one group however
-    # many ensembles and frames the run decodes.  Ensemble 0 of rank 0 is generated with
-    # its transmitted bits (the checked step compares the decoded MSC/FIC bits with them).
+    threads = min(16, os.cpu_count() or 1)
+    # Every stream is cyclic (dabsynth_generate_period: P frames repeated end to end, a
+    # valid DAB stream across the seams); ensemble 0 of each rank is generated with its
+    # transmitted bits for the checked step.
     t0 = time.time()
     diq = ctx.buf(E * 2 * stride * 4)
-    truth = None
-    seed0 = rank_seed0(0 if rccl else rank, E)
+    seed0 = rank_seed0(rank, E)
     cs, nchunks = chunk_layout(stride, F)
-    src16 = None
-    if rccl and rank == 0:
+    truth = ens.generate_period(seed0, P, truth=True)
+    truth.pop("iq")
+    split = None
+    if rccl:
         import torch
-        # rank 0's pool as int16, chunk-major [chunk][ensemble][2*cs]: chunk k of every
-        # stream is one contiguous message per destination rank
-        src16 = torch.zeros((nchunks, E, 2 * cs), dtype=torch.int16, device=f"cuda:{rank_device(local)}")
-    group = 8
-    if rank == 0 or not rccl:
-        for g0 in range(0, E, group):
-            n = min(group, E - g0)
-            if g0 == 0 and rank == 0:
-                import threading
-                box = {}
-                th = threading.Thread(target=lambda: box.update(g=ens.generate(seed0, truth=True)))
-                th.start()
-                rest = ens.generate_many(n - 1, seed0=seed0 + 1, threads=min(16, os.cpu_count() or 1))
-                th.join()
-                truth = box["g"]
-                part = np.concatenate([truth["iq"][None, :], rest])
-                del rest
-            else:
-                part = ens.generate_many(n, seed0=seed0 + g0, threads=min(16, os.cpu_count() or 1))
-            if src16 is not None:
-                p16 = np.zeros((n, nchunks * 2 * cs), np.int16)
-                p16[:, :2 * stride] = to_s16(part)
-                src16[:, g0:g0 + n] = torch.from_numpy(p16.reshape(n, nchunks, 2 * cs).transpose(1, 0, 2).copy()).to(
-                    src16.device)
-                part = p16[:, :2 * stride].astype(np.float32) / 32768.0   # what the receivers decode
-                del p16
-            diq.upload_at(part, g0 * 2 * stride * 4)
-            del part
+        dev = f"cuda:{rank_device(local)}"
+        src = None
+        if rank == 0:
+            # rank 0 holds every rank's streams as int16 (.sdr samples), one period each,
+            # as the P / F distinct chunk phases [phase][ensemble][2 * cs]
+            src = [torch.from_numpy(chunk_phases(ens, P, cs, E, rank_seed0(r, E), threads)).to(dev)
+                   for r in range(world)]
+        split = StreamSplit(dist, rank, world, E, cs, P // F, nchunks, dev, src)
+    else:
+        for g0 in range(0, E, 8):
+            n = min(8, E - g0)
+            per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
+            for e in range(n):
+                for p, q, m in ens.stream_pieces(P):
+                    diq.upload_at(per[e, 2 * q:2 * (q + m)], ((g0 + e) * 2 * stride + 2 * p) * 4)
+            del per
     gen_s = time.time() - t0
     subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, dabamd.SUBCH_DABPLUS if s[5] else 0)
             for s in SUBCH]
     pipe = dabamd.Pipeline(ctx, E, F, subs)
 
-    # stream split over RCCL: chunk k of every stream from rank 0 to each rank
-    feed = None
+    # stream split over RCCL: chunk k of every stream from rank 0 to each rank, converted
+    # into this rank's cf32 stream buffer on the GPU
+    got = [0]                                             # chunks available on this rank
+
+    def feed_end(k, reqs):
+        chunk = split.end(k, reqs)
+        if chunk is None:
+            return
+        m = min(cs, stride - k * cs)
+        for e in range(E):
+            ctx.iq_convert(dabamd.IQ_S16, _TorchBuf(chunk[e]), m, diq, dst_off=(e * 2 * stride + 2 * k * cs) * 4)
+        ctx.sync()                                        # the receive buffer is reused by the next chunk
+        got[0] = k + 1
     if rccl:
-        import torch
-        dev = f"cuda:{rank_device(local)}"
-        recv = torch.zeros((E, 2 * cs), dtype=torch.int16, device=dev) if rank else None
-        got = [0]                                         # chunks available on this rank
-
-        def feed_begin(k):
-            """start moving chunk k of every stream from rank 0 to each rank"""
-            if k >= nchunks:
-                return None
-            return scatter_chunk(dist, rank, world, [src16[k]] * world if rank == 0 else None, recv)
-
-        def feed_end(k, reqs):
-            """wait for chunk k and convert it into this rank's cf32 stream buffer"""
-            if reqs is None:
-                return
-            for r in reqs:
-                r.wait()
-            if rank:
-                torch.cuda.current_stream().synchronize()
-                m = min(cs, stride - k * cs)
-                for e in range(E):
-                    ctx.iq_convert(dabamd.IQ_S16, _TorchBuf(recv[e]), m, diq,
-                                   dst_off=(e * 2 * stride + 2 * k * cs) * 4)
-                ctx.sync()                                # recv is reused by the next chunk
-            got[0] = k + 1
-        feed = (feed_begin, feed_end)
+        torch.cuda.synchronize()
         for k in range(2):
-            feed_end(k, feed_begin(k))
+            feed_end(k, split.begin(k))
 
     def avail():
         if not rccl:
@@ -428,11 +503,11 @@ def main():
 
     def step(k, download=False):
         # chunk k + 2 travels while step k decodes (the frames of step k need chunks <= k + 1)
-        reqs = feed[0](k + 2) if feed is not None else None
+        reqs = split.begin(k + 2) if rccl else None
         r = pipe.run(diq, stride, avail(), download=download)
         d = pipe.dabplus(download=download) if dabplus else None
-        if feed is not None:
-            feed[1](k + 2, reqs)
+        if rccl:
+            feed_end(k + 2, reqs)
         return r, d
 
     for i in range(args.warmup):
@@ -456,29 +531,16 @@ def main():
     tm = {k: (v[0] / args.steps, v[0] / max(v[1], 1)) for k, v in tsum.items()}
 
     # one extra step (outside the timed region) whose outputs are checked against the
-    # transmitted bits of ensemble 0 (rank 0): every FIB CRC, every MSC subchannel
+    # transmitted bits of ensemble 0 of every rank: every FIB, every MSC subchannel
     ck = args.warmup + args.steps
     st0 = pipe.state(0)
     (fic, crc, msc, valid), dp = step(ck, download=True)
-    check = None
-    if rank == 0 and truth is not None:
-        st1 = pipe.state(0)
-        f0 = st1.frames_run
-        cif0 = st0.cif_count
-        g_frame0 = (cif0 // 4)
-        flip = _crc_flip()
-        fic_ok = all(np.array_equal(fic[0, f, b] ^ flip, truth["fic"][g_frame0 + f, b])
-                     for f in range(f0) for b in range(4))
-        msc_ok = msc_n = 0
-        for c in range(4 * f0):
-            if not valid[0, c]:
-                continue
-            for k, sc in enumerate(SUBCH):
-                nb = 24 * sc[2]
-                msc_n += 1
-                msc_ok += int(np.array_equal(msc[0, c, k, :nb], truth["msc"][cif0 + c, k, :nb]))
-        check = {"ensemble": 0, "frames": int(f0), "fic_blocks_equal_transmitted": bool(fic_ok),
-                 "fic_crc_pass_rate": float(crc.mean()), "msc_codewords": msc_n, "msc_equal_transmitted": msc_ok}
+    # every rank checks its ensemble 0 against the transmitted bits; rank 0 reports all
+    st1 = pipe.state(0)
+    check = check_step(truth, P, st0, st1, fic, crc, msc, valid, SUBCH)
+    check["rank"] = rank
+    check["seed"] = seed0
+    checks = gather_objects(dist, check)
     # the same workload with every kernel alone (after the measurement: never timed)
     tm_alone = {}
     if args.solo_steps > 0:
@@ -498,12 +560,12 @@ def main():
 
     symbols = world * E * F * 76 * args.steps
     value = symbols / el
-    split = None
+    probe = None
     if world > 1 and not rccl:
         try:
-            split = stream_split_probe(dist, rank, world, local, E, F)
+            probe = stream_split_probe(dist, rank, world, local, E, F)
         except Exception as e:                          # never costs the main measurement
-            split = {"error": repr(e)[:300]}
+            probe = {"error": repr(e)[:300]}
     if rank != 0:
         return
     # dominant kernel + its roofline.  Launches overlap in the pipeline (the next run's
@@ -561,12 +623,16 @@ def main():
         "kernel_ms_per_launch": {k: v[1] for k, v in tm.items()},
         "kernel_ms_per_launch_alone": tm_alone,
         "kernel_timing": "HIP events on each launch's stream over the timed steps (rocprofv3 --kernel-trace agrees)",
-        "checked_step": check,
+        "checked_step": checks[0] if world == 1 else checks,
         "dabplus_last_step": sf_ok,
         "gen_seconds": gen_s,
     }
-    if split is not None:
-        out["stream_split"] = split
+    if probe is not None:
+        out["stream_split"] = probe
+    if rccl:
+        out["stream_split"] = {"mode": "fed end to end: rank 0 -> every rank, grouped send/recv per step chunk",
+                               "backend": dist.get_backend(), "distinct_ensembles": world * E,
+                               "bytes_per_rank_per_step": E * 2 * cs * 2}
     if cpu is not None:
         t = cpu["tot"]
         out["cpu_baseline"] = {

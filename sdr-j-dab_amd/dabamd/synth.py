@@ -33,6 +33,8 @@ def lib() -> C.CDLL:
         _lib.dabsynth_stream_len.argtypes = [C.c_void_p]
         _lib.dabsynth_generate.argtypes = [C.c_void_p, C.c_uint64] + [C.c_void_p] * 5
         _lib.dabsynth_generate_many.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int] + [C.c_void_p] * 3
+        _lib.dabsynth_generate_period.argtypes = [C.c_void_p, C.c_uint64, C.c_int] + [C.c_void_p] * 3
+        _lib.dabsynth_period_many.argtypes = [C.c_void_p, C.c_uint64, C.c_int, C.c_int, C.c_int, C.c_void_p]
         _lib.dabsynth_conv_encode.argtypes = [C.c_void_p, C.c_int, C.c_void_p]
         _lib.dabsynth_puncture_msc.argtypes = [C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
         _lib.dabsynth_rs_encode.argtypes = [C.c_void_p, C.c_void_p]
@@ -74,6 +76,51 @@ class Ensemble:
         rc = lib().dabsynth_generate_many(C.byref(self.cfg), seed0, n_ens, threads, _p(iq), None, None)
         if rc:
             raise DabError(f"dabsynth_generate_many failed {rc}")
+        return iq
+
+    # ---- cyclic streams (dabsynth_generate_period) ----------------------------------
+    def generate_period(self, seed: int, period: int, truth: bool = True):
+        """One period (`period` frames from frame 0's null) of a cyclic stream; truth
+        arrays indexed by frame mod period / receiver CIF mod 4*period."""
+        TF = 196608
+        iq = np.zeros(2 * period * TF, dtype=np.float32)
+        NS = len(self.subch)
+        fic = np.zeros((period, 4, 768), np.uint8) if truth else None
+        msc = np.zeros((4 * period, NS, self.maxbits), np.uint8) if truth and NS else None
+        rc = lib().dabsynth_generate_period(C.byref(self.cfg), seed, period, _p(iq), _p(fic), _p(msc))
+        if rc:
+            raise DabError(f"dabsynth_generate_period failed {rc}")
+        return dict(iq=iq, fic=fic, msc=msc, period=period)
+
+    def period_many(self, n_ens: int, seed0: int, period: int, threads: int = 8) -> np.ndarray:
+        iq = np.zeros((n_ens, 2 * period * 196608), dtype=np.float32)
+        rc = lib().dabsynth_period_many(C.byref(self.cfg), seed0, period, n_ens, threads, _p(iq))
+        if rc:
+            raise DabError(f"dabsynth_period_many failed {rc}")
+        return iq
+
+    def period_offset(self) -> int:
+        """stream sample of period sample 0 (frame 0's null start): TF - pre_offset"""
+        return 196608 - self.cfg.pre_offset
+
+    def stream_pieces(self, period: int, p0: int = 0, n: Optional[int] = None):
+        """(stream sample, period sample, count) runs covering stream samples [p0, p0 + n)
+        of the cyclic stream (default: the whole stream of this Ensemble's length)"""
+        L = period * 196608
+        n = self.length - p0 if n is None else n
+        out, p, end = [], p0, p0 + n
+        while p < end:
+            q = (p - self.period_offset()) % L
+            m = min(end - p, L - q)
+            out.append((p, q, m))
+            p += m
+        return out
+
+    def stream_from_period(self, period_iq: np.ndarray, period: int) -> np.ndarray:
+        """the whole cyclic stream (this Ensemble's length) from one period"""
+        iq = np.empty(2 * self.length, np.float32)
+        for p, q, m in self.stream_pieces(period):
+            iq[2 * p:2 * (p + m)] = period_iq[2 * q:2 * (q + m)]
         return iq
 
 

@@ -395,22 +395,29 @@ int64_t dabsynth_stream_len(const dabsynth_cfg *cfg) {
     return (int64_t)(TF - cfg->pre_offset) + (int64_t)cfg->n_frames * TF + TNULL;
 }
 
-int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
-                      uint8_t *fic_bits, uint8_t *msc_bits, uint8_t *coded_bits,
-                      int64_t *frame0_start) {
+// The transmitter.  P == 0: a linear stream of dabsynth_stream_len samples (pre-roll
+// frame -1, frames 0..F-1, a closing null; encoder CIFs from -19 so the receiver's
+// CIF 16 onwards decodes).  P > 0: one period of a cyclic stream, P frames of TF
+// samples starting at frame 0's null: the time interleaver and the DAB+ superframe
+// grid wrap around the period, so the period repeated end to end is a valid stream
+// everywhere (truth: receiver CIF n decodes encoder CIF (n - 15) mod 4P).
+static int gen_core(const dabsynth_cfg *cfg, uint64_t seed, int P, float *iq, uint8_t *fic_bits,
+                    uint8_t *msc_bits, uint8_t *coded_bits, int64_t *frame0_start) {
     const Tables &t = T();
-    const int F = cfg->n_frames, NS = cfg->n_subch;
-    if (F < 0 || cfg->pre_offset < 0 || cfg->pre_offset >= TF) return -1;
+    const bool cyc = P > 0;
+    const int F = cyc ? P : cfg->n_frames, NS = cfg->n_subch;
+    if (F < 0 || (!cyc && (cfg->pre_offset < 0 || cfg->pre_offset >= TF))) return -1;
     Rng rng(seed);
     int maxbr = 8;
     for (int s = 0; s < NS; s++) maxbr = std::max<int>(maxbr, cfg->subch[s].bitRate);
-    // encoder CIFs e in [-19, 4F): index e + 19
-    const int NE = 4 * F + 19;
+    // encoder CIFs e in [e0, 4F): slot e - e0
+    const int e0 = cyc ? 0 : -19, NE = 4 * F - e0, NC = 4 * F;
     std::vector<std::vector<uint8_t>> enc_frag(NS);      // punctured bits per (e, s)
     std::vector<int> frag_len(NS);
     for (int s = 0; s < NS; s++) {
         const dabsynth_subch &sc = cfg->subch[s];
         int nb = 24 * sc.bitRate;
+        if (cyc && sc.dabplus && NC % 5) return -3;      // superframes must tile the period
         frag_len[s] = sc.length * 64;
         enc_frag[s].assign((size_t)NE * frag_len[s], 0);
         std::vector<uint8_t> info(nb), mother(4 * (nb + 6)), punct(frag_len[s] + 64);
@@ -419,9 +426,9 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
         // dabplus = 1 + k: the superframe grid is shifted by k CIFs (k = 1..4 makes the
         // receiver's first five CIFs straddle two superframes)
         int sf_pos = sc.dabplus > 1 ? ((sc.dabplus - 1) % 5) * (nb / 8) : 0;
-        for (int e = -19; e < 4 * F; e++) {
+        for (int e = e0; e < NC; e++) {
             if (sc.dabplus) {
-                // 5 CIFs carry one superframe; superframes start at e = -19 + 5m
+                // 5 CIFs carry one superframe; superframes start at e = e0 + 5m
                 int per = nb / 8;
                 for (int byte = 0; byte < per; byte++) {
                     if (sf_pos == 0) make_superframe(rng, rsdims, sf.data());
@@ -432,8 +439,8 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
             } else {
                 for (int i = 0; i < nb; i++) info[i] = rng.bit();
             }
-            int n = e + 15;                                  // receiver CIF decoding this
-            if (msc_bits && n >= 0 && n < 4 * F)
+            int n = cyc ? (e + 15) % NC : e + 15;           // receiver CIF decoding this
+            if (msc_bits && n >= 0 && n < NC)
                 for (int i = 0; i < nb; i++)
                     msc_bits[((size_t)n * NS + s) * (24 * maxbr) + i] = info[i];
             std::vector<uint8_t> scr(nb);
@@ -442,29 +449,29 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
             std::fill(punct.begin(), punct.end(), 0);
             int np = dabsynth_puncture_msc(sc.uep, sc.bitRate, sc.protLevel, mother.data(), punct.data());
             if (np < 0 || np > frag_len[s]) return -2;
-            std::memcpy(&enc_frag[s][(size_t)(e + 19) * frag_len[s]], punct.data(), frag_len[s]);
+            std::memcpy(&enc_frag[s][(size_t)(e - e0) * frag_len[s]], punct.data(), frag_len[s]);
         }
     }
-    // the stream: pre-roll frame (index -1) then F frames, then one null
-    const int64_t total = dabsynth_stream_len(cfg);
+    // linear: the pre-roll frame (index -1) then F frames, then one null; cyclic: F frames
+    const int64_t total = cyc ? (int64_t)P * TF : dabsynth_stream_len(cfg);
     const double amp = cfg->amplitude > 0 ? cfg->amplitude : 1.0;
     const double scale = amp / std::sqrt((double)K);
     const bool noisy = cfg->snr_db < 200.0f;
     const double sigma = noisy ? amp * std::pow(10.0, -cfg->snr_db / 20.0) / std::sqrt(2.0) : 0.0;
-    const int64_t base = -(int64_t)cfg->pre_offset;   // stream index of pre-roll frame start
+    const int64_t base = cyc ? -(int64_t)TF : -(int64_t)cfg->pre_offset;   // stream index of frame -1
     if (frame0_start) *frame0_start = base + TF;
     std::vector<uint8_t> symbits(3072);
     std::vector<int> phase(TU);
     std::vector<double> zr(TU), zi(TU), xr(TU), xi(TU);
     uint64_t fib_state = seed ^ 0xF1B0F1B0ull;
-    for (int f = -1; f < F; f++) {
+    for (int f = cyc ? 0 : -1; f < F; f++) {
         int64_t fstart = base + (int64_t)(f + 1) * TF;
         // FIC: 4 blocks x 3 FIBs -> 9216 punctured bits over symbols 1..3
         std::vector<uint8_t> ficsym(9216);
         for (int blk = 0; blk < 4; blk++) {
             uint8_t fib[768], mother[3096], punct[2304];
             for (int q = 0; q < 3; q++) {
-                if (cfg->figs) make_fig_fib(cfg, ((int64_t)(f + 1) * 4 + blk) * 3 + q, fib + 256 * q);
+                if (cfg->figs) make_fig_fib(cfg, ((int64_t)(f + (cyc ? 0 : 1)) * 4 + blk) * 3 + q, fib + 256 * q);
                 else dabsynth_make_fib(&fib_state, fib + 256 * q);
             }
             if (fic_bits && f >= 0) std::memcpy(&fic_bits[((size_t)f * 4 + blk) * 768], fib, 768);
@@ -492,7 +499,8 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
                                 int rv = ((br & 1) << 3) | ((br & 2) << 1) | ((br & 4) >> 1) | ((br & 8) >> 3);
                                 int d = 15 - rv;            // receiver delay
                                 int e = m - (15 - d);
-                                v = (e >= -19) ? enc_frag[s][(size_t)(e + 19) * frag_len[s] + j] : 0;
+                                if (cyc) e = (e + NC) % NC;
+                                v = (e >= e0) ? enc_frag[s][(size_t)(e - e0) * frag_len[s] + j] : 0;
                             }
                         }
                         symbits[i] = v;
@@ -529,6 +537,8 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
     }
     for (int64_t p = base + (int64_t)(F + 1) * TF; p < total; p++)
         if (p >= 0) iq[2 * p] = iq[2 * p + 1] = 0.0f;
+    // the carrier offset's phase restarts with each period: the step falls in frame 0's
+    // null symbol, where a receiver's NCO sees no signal
     if (noisy || cfg->cfo_hz != 0.0f) {
         for (int64_t p = 0; p < total; p++) {
             double re = iq[2 * p], im = iq[2 * p + 1];
@@ -542,6 +552,35 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
             iq[2 * p] = (float)re; iq[2 * p + 1] = (float)im;
         }
     }
+    return 0;
+}
+
+int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
+                      uint8_t *fic_bits, uint8_t *msc_bits, uint8_t *coded_bits,
+                      int64_t *frame0_start) {
+    return gen_core(cfg, seed, 0, iq, fic_bits, msc_bits, coded_bits, frame0_start);
+}
+
+int dabsynth_generate_period(const dabsynth_cfg *cfg, uint64_t seed, int period, float *iq,
+                             uint8_t *fic_bits, uint8_t *msc_bits) {
+    if (period < 4) return -1;
+    return gen_core(cfg, seed, period, iq, fic_bits, msc_bits, nullptr, nullptr);
+}
+
+int dabsynth_period_many(const dabsynth_cfg *cfg, uint64_t seed0, int period, int n_ens, int n_threads,
+                         float *iq) {
+    const size_t len = (size_t)period * TF;
+    if (n_threads < 1) n_threads = 1;
+    std::vector<int> rc(n_ens, 0);
+    std::vector<std::thread> pool;
+    for (int w = 0; w < n_threads; w++)
+        pool.emplace_back([&, w]() {
+            for (int e = w; e < n_ens; e += n_threads)
+                rc[e] = dabsynth_generate_period(cfg, seed0 + (uint64_t)e, period, iq + (size_t)e * 2 * len,
+                                                 nullptr, nullptr);
+        });
+    for (auto &th : pool) th.join();
+    for (int e = 0; e < n_ens; e++) if (rc[e]) return rc[e];
     return 0;
 }
 

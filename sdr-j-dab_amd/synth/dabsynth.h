@@ -63,6 +63,19 @@ int dabsynth_generate(const dabsynth_cfg *cfg, uint64_t seed, float *iq,
 int dabsynth_generate_many(const dabsynth_cfg *cfg, uint64_t seed0, int n_ens, int n_threads,
                            float *iq, uint8_t *fic_bits, uint8_t *msc_bits);
 
+/* One period of a cyclic stream: P frames (P >= 4) of TF samples, frame 0's null
+ * symbol first.  The time interleaver (and the DAB+ superframe grid: 4P must then be a
+ * multiple of 5) wraps around the period, so the period repeated end to end is a valid
+ * stream anywhere.  A stream of any length with the linear generator's layout (frame 0
+ * at TF - pre_offset) is iq_stream[p] = iq[(p - (TF - pre_offset)) mod (P * TF)].
+ * Truth: fic_bits [P][4][768] by frame; msc_bits [4P][n_subch][24*max_bitRate] by
+ * receiver CIF n mod 4P (receiver CIF n decodes encoder CIF (n - 15) mod 4P). */
+int dabsynth_generate_period(const dabsynth_cfg *cfg, uint64_t seed, int period, float *iq,
+                             uint8_t *fic_bits, uint8_t *msc_bits);
+/* periods of n_ens ensembles (seeds seed0 + e) in parallel: iq [n_ens][2 * period * TF] */
+int dabsynth_period_many(const dabsynth_cfg *cfg, uint64_t seed0, int period, int n_ens, int n_threads,
+                         float *iq);
+
 /* building blocks exposed for tests */
 void dabsynth_conv_encode(const uint8_t *bits, int nbits, uint8_t *coded /*[4*(nbits+6)]*/);
 int  dabsynth_puncture_msc(int uep, int bitRate, int protLevel, const uint8_t *mother, uint8_t *out);

@@ -3,10 +3,11 @@
 Covers what the N-GPU bench relies on: torch.distributed rendezvous from the
 launcher's env vars, the start/stop barrier, the max-over-ranks time, the disjoint
 per-rank ensemble seeds (rank-local mode: each rank decodes its own ensembles) and
-the C4 stream split (--iq-source rccl): rank 0 holds the int16 IQ of the ranks'
-ensembles in the chunk-major layout and scatters each chunk with one grouped
-send/recv; every rank must receive its own streams byte-identical, and the
-received chunks, converted back, must decode (oracle) like the rank's own IQ."""
+the C4 stream split (--iq-source rccl) through the bench's own code
+(bench.chunk_phases + bench.StreamSplit): rank 0 holds every rank's cyclic int16
+streams and sends each rank chunk k of its OWN ensembles per step; every rank must
+receive exactly its own streams, which must decode (oracle) to its own transmitted
+FIBs, and the per-rank checks gather on every rank."""
 import os
 import socket
 import sys
@@ -56,32 +57,39 @@ def _split_worker(rank, world, port, q):
     import oracle_py as orc
     from dabamd.synth import Ensemble
     r, local, w, dist = bench.dist_setup(world)
-    E, F = 2, 1
-    ens = Ensemble(3, snr_db=300.0)
+    E, F = 2, 2
+    ens = Ensemble(7, snr_db=30.0)
     stride = ens.length
+    P = bench.period_frames(F, False)
     cs, nchunks = bench.chunk_layout(stride, F)
-
-    def chunked(seed0):
-        iq = ens.generate_many(E, seed0=seed0, threads=2)
-        p16 = np.zeros((E, nchunks * 2 * cs), np.int16)
-        p16[:, :2 * stride] = bench.to_s16(iq)
-        return torch.from_numpy(p16.reshape(E, nchunks, 2 * cs).transpose(1, 0, 2).copy())
-    # rank 0 holds every rank's streams ([rank][chunk][ensemble][2*cs]); rank r decodes
-    # the ensembles of seed rank_seed0(r)
-    src = [chunked(bench.rank_seed0(d, E)) for d in range(world)] if rank == 0 else None
-    recv = torch.zeros((E, 2 * cs), dtype=torch.int16)
+    # the bench's own feed: rank 0 holds every rank's cyclic streams as chunk phases and
+    # sends each rank its own chunk k per step (bench.StreamSplit)
+    src = [torch.from_numpy(bench.chunk_phases(ens, P, cs, E, bench.rank_seed0(d, E), 2)) for d in range(world)] \
+        if rank == 0 else None
+    split = bench.StreamSplit(dist, rank, world, E, cs, P // F, nchunks, "cpu", src)
     got = np.zeros((E, nchunks * 2 * cs), np.int16)
-    for k in range(nchunks):
-        reqs = bench.scatter_chunk(dist, rank, world, [src[d][k] for d in range(world)] if rank == 0 else None, recv)
-        for q_ in reqs:
-            q_.wait()
-        got[:, 2 * k * cs:2 * (k + 1) * cs] = (src[0][k] if rank == 0 else recv).numpy()
-    mine = chunked(bench.rank_seed0(rank, E)).numpy().transpose(1, 0, 2).reshape(E, -1)
-    same = bool(np.array_equal(got, mine))
+    for k in range(nchunks + 1):                          # one call past the end: None
+        chunk = split.end(k, split.begin(k))
+        if k == nchunks:
+            assert chunk is None
+            break
+        got[:, 2 * k * cs:2 * (k + 1) * cs] = chunk.numpy()
+    seed0 = bench.rank_seed0(rank, E)
+    per = ens.period_many(E, seed0=seed0, period=P, threads=2)
+    mine = np.stack([bench.to_s16(ens.stream_from_period(per[e], P)) for e in range(E)])
+    same = bool(np.array_equal(got[:, :2 * stride], mine))
+    # the received samples decode to this rank's own transmitted bits
+    truth = ens.generate_period(seed0, P, truth=True)
     iq = got[0, :2 * stride].astype(np.float32) / 32768.0
-    n, info, soft = orc.ofdm_run(iq, 2)
+    ref = orc.decode_stream(iq, 7, [])
+    flip = np.zeros(768, np.uint8)
+    for b in range(3):
+        flip[256 * b + 240:256 * b + 256] = 1
+    fic_ok = ref["n"] >= 6 and ref["crc"][:ref["n"]].all() and all(
+        np.array_equal(ref["fic"][f, b] ^ flip, truth["fic"][f % P, b]) for f in range(ref["n"]) for b in range(4))
     bench.barrier(dist)
-    q.put((rank, same, n, hash(got.tobytes())))
+    checks = bench.gather_objects(dist, {"rank": rank, "fic_ok": bool(fic_ok)})
+    q.put((rank, same, bool(fic_ok), hash(got.tobytes()), checks))
     dist.destroy_process_group()
 
 
@@ -96,10 +104,11 @@ def test_stream_split_scatter_gloo():
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, same0, n0, h0), (r1, same1, n1, h1) = res
+    (r0, same0, ok0, h0, c0), (r1, same1, ok1, h1, c1) = res
     assert same0 and same1                   # every rank got exactly its own streams
-    assert n0 == n1 == 2                     # and they decode
+    assert ok0 and ok1                       # which decode to its own transmitted FIBs
     assert h0 != h1                          # disjoint ensembles per rank
+    assert c0 == c1 == [{"rank": 0, "fic_ok": True}, {"rank": 1, "fic_ok": True}]   # gathered checks
 
 
 def test_two_ranks_gloo():
