@@ -13,7 +13,10 @@ _lib: Optional[C.CDLL] = None
 
 class SynthSubch(C.Structure):
     _fields_ = [("startAddr", C.c_int16), ("length", C.c_int16), ("bitRate", C.c_int16),
-                ("protLevel", C.c_int16), ("uep", C.c_int16), ("dabplus", C.c_int16)]
+                ("protLevel", C.c_int16), ("uep", C.c_int16), ("dabplus", C.c_int16), ("content", C.c_int16)]
+
+
+MP2, PACKET = 2, 3   # SynthSubch.content (dabsynth.h DABSYNTH_MP2 / DABSYNTH_PACKET)
 
 
 class SynthCfg(C.Structure):
@@ -47,7 +50,8 @@ def _p(a):
 
 class Ensemble:
     """Synthetic ensemble generator.  subch: tuples (startAddr, length, bitRate,
-    protLevel, uep, dabplus) -- uep=1 for UEP (uepFlag 0 in the reference)."""
+    protLevel, uep, dabplus[, content]) -- uep=1 for UEP (uepFlag 0 in the reference);
+    content MP2 / PACKET for MPEG layer II frames / packet-mode data groups."""
 
     def __init__(self, n_frames: int, subch: Sequence[tuple] = (), pre_offset: int = 50000,
                  snr_db: float = 300.0, cfo_hz: float = 0.0, amplitude: float = 1.0, figs: bool = False):

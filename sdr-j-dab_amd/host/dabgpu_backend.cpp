@@ -152,9 +152,8 @@ bool mp4Processor::processSuperframe(int base) {                 // mp4processor
 // ---- dabConcurrent / mscDatagroup ---------------------------------------------------
 dabConcurrent::dabConcurrent(uint8_t dabModus, int16_t fragmentSize, int16_t bitRate, int16_t uepFlag,
                              int16_t protLevel, std::unique_ptr<dabProcessor> processor)
-    : fragmentSize_(fragmentSize), bitRate_(bitRate), delay_((size_t)16 * fragmentSize, 0), data_(fragmentSize),
-      outV_((size_t)24 * bitRate), proc_(std::move(processor)) {
-    (void)dabModus;
+    : dabModus_(dabModus), fragmentSize_(fragmentSize), bitRate_(bitRate), delay_((size_t)16 * fragmentSize, 0),
+      data_(fragmentSize), outV_((size_t)24 * bitRate), proc_(std::move(processor)) {
     sub_ = dabgpu_subch{0, (int16_t)(fragmentSize / 64), bitRate, protLevel, uepFlag, 0};
     int32_t nb, fr, ns, L[4], PI[4];
     chk(dabgpu_subch_profile(&sub_, &nb, &fr, &ns, L, PI) < 0 ? DABGPU_E_UNSUP : DABGPU_OK,
@@ -189,6 +188,11 @@ int32_t dabConcurrent::process(int16_t *v, int16_t cnt) {
     if (cnt != fragmentSize_) throw error(DABGPU_E_ARG, "dabConcurrent::process: fragment size");
     if (deinterleave(v) && proc_) proc_->addtoFrame(outV_.data(), (int16_t)(24 * bitRate_));
     return cnt;
+}
+
+void dabConcurrent::setFiles(FILE *mp2, FILE *mp4) {                // dab-concurrent.cpp:196-200
+    (void)mp4;
+    if (dabModus_ == DAB && proc_) proc_->setFile(mp2);
 }
 
 mscDatagroup::mscDatagroup(uint8_t DSCTy, int16_t packetAddress, int16_t fragmentSize, int16_t bitRate,
@@ -240,7 +244,7 @@ void mscHandler::process_mscBlock(int16_t *fbits, int16_t blkno) { // msc-handle
             const uint8_t modus = na_.ASCTy == 077 ? DAB_PLUS : DAB;
             std::unique_ptr<dabProcessor> proc;
             if (modus == DAB_PLUS) proc.reset(new mp4Processor(na_.bitRate, out_.aac));
-            else proc.reset(new mp2Processor(na_.bitRate, out_.mp2));
+            else proc.reset(new mp2Processor(na_.bitRate, out_.mp2, mp2File_));   // msc-handler.cpp:147-150
             dabHandler_.reset(new dabConcurrent(modus, (int16_t)(na_.length * 64), na_.bitRate, na_.uepFlag,
                                                 na_.protLevel, std::move(proc)));
             startAddr_ = na_.startAddr;
@@ -267,5 +271,11 @@ void mscHandler::stop() {
     dabHandler_->stop();
 }
 void mscHandler::stopProcessing() { work_to_be_done_ = false; }
+void mscHandler::setFiles(FILE *mp2, FILE *mp4) {                  // msc-handler.cpp:208-212
+    std::lock_guard<std::mutex> g(locker_);
+    mp2File_ = mp2;
+    mp4File_ = mp4;
+    dabHandler_->setFiles(mp2, mp4);
+}
 
 }  // namespace dabgpu

@@ -139,14 +139,24 @@ int32_t phaseReference::findIndex(DSPCOMPLEX *v) {
 }
 
 // ---- ficHandler -------------------------------------------------------------------
-ficHandler::ficHandler(fib_cb cb, int16_t bitsperBlock) : cb_(std::move(cb)), ofdm_input_(2304) {
+ficHandler::ficHandler(signals sig, int16_t bitsperBlock) : sig_(std::move(sig)) {
+    init(bitsperBlock);
+    fibProcessor_.on_ensemble(sig_.nameofEnsemble);
+    fibProcessor_.on_service(sig_.addtoEnsemble);
+}
+
+ficHandler::ficHandler(fib_cb cb, int16_t bitsperBlock) : cb_(std::move(cb)) { init(bitsperBlock); }
+
+void ficHandler::init(int16_t bitsperBlock) {
     if (bitsperBlock != 2 * DABGPU_K) throw error(DABGPU_E_UNSUP, "ficHandler: Mode I (3072 bits per block) only");
+    ofdm_input_.assign(2304, 0);
     in_.resize(sizeof(int16_t) * 2304);
     bits_.resize(768);
     crc_.resize(16);
 }
 
 void ficHandler::process_ficBlock(int16_t *data, int16_t blkno) {   // fic-handler.cpp:192-224
+    if (!running_.load()) return;
     if (blkno == 1) {
         index_ = 0;
         ficno_ = 0;
@@ -162,11 +172,17 @@ void ficHandler::process_ficBlock(int16_t *data, int16_t blkno) {   // fic-handl
             uint8_t bits[768], ok[3];
             bits_.download(bits, 768);
             crc_.download(ok, 3);
-            for (int k = 0; k < 3; k++) {
-                total_++;
-                good_ += ok[k] ? 1 : 0;
-                if (cb_) cb_(bits + 256 * k, ok[k] != 0, (int16_t)ficno_);
+            {
+                std::lock_guard<std::mutex> g(fibHandling_);          // fic-handler.cpp:304-320
+                for (int k = 0; k < 3; k++) {
+                    total_++;
+                    good_ += ok[k] ? 1 : 0;
+                    if (sig_.show_ficCRC) sig_.show_ficCRC(ok[k] != 0);
+                    if (ok[k]) fibProcessor_.process_FIB(bits + 256 * k, (uint16_t)ficno_);
+                }
             }
+            for (int k = 0; k < 3; k++)
+                if (cb_) cb_(bits + 256 * k, ok[k] != 0, (int16_t)ficno_);
             index_ = 0;
             ficno_++;
         }
@@ -174,6 +190,28 @@ void ficHandler::process_ficBlock(int16_t *data, int16_t blkno) {   // fic-handl
 }
 
 int16_t ficHandler::get_ficRatio() const { return total_ ? (int16_t)(100 * good_ / total_) : 0; }
+
+void ficHandler::clearEnsemble() {                                   // fic-handler.cpp:159-163
+    std::lock_guard<std::mutex> g(fibHandling_);
+    fibProcessor_.clearEnsemble();
+}
+
+uint8_t ficHandler::kindofService(const std::string &s) {           // fic-handler.cpp:165-171
+    std::lock_guard<std::mutex> g(fibHandling_);
+    return fibProcessor_.kindofService(s);
+}
+
+void ficHandler::dataforAudioService(const std::string &s, audiodata *d) {   // :174-178
+    std::lock_guard<std::mutex> g(fibHandling_);
+    (void)fibProcessor_.dataforAudioService(s, d);
+}
+
+void ficHandler::dataforDataService(const std::string &s, packetdata *d) {   // :180-184
+    std::lock_guard<std::mutex> g(fibHandling_);
+    (void)fibProcessor_.dataforDataService(s, d);
+}
+
+void ficHandler::stop() { running_.store(false); }                  // fic-handler.cpp:155-157
 
 // ---- ensembleDecoder -------------------------------------------------------------
 ensembleDecoder::ensembleDecoder(const config &cfg) : cfg_(cfg) {

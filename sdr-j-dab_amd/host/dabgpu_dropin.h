@@ -141,21 +141,53 @@ private:
     devbuf iq_, fr_, si_;
 };
 
-// ficHandler without Qt (fic-handler.cpp:143-321): process_ficBlock accumulates
-// symbols 1..3 of a frame into the 4 FIC blocks, decodes each on the GPU and
-// hands every FIB (256 bits, CRC field inverted as check_CRC_bits leaves it)
-// with its CRC verdict to the callback that stands in for fibProcessor::process_FIB.
+// ficHandler without Qt (fic-handler.cpp:143-321, fic-handler.h:44-52): process_ficBlock
+// accumulates symbols 1..3 of a frame into the 4 FIC blocks and decodes each on the GPU
+// (depuncture, Viterbi, energy dispersal, CRC); every CRC-good FIB goes to the owned
+// fib_processor under the fibHandling lock, as process_ficInput does (:304-320), so the
+// GUI's service lookups (kindofService, dataforAudioService, dataforDataService,
+// clearEnsemble) work on this class as on the reference's.  QString& arguments are
+// std::string (UTF-8, the 16 characters of the label as transmitted).  Signals are
+// callbacks: show_ficCRC per FIB, nameofEnsemble / addtoEnsemble from the FIG parser.
+// Optionally every FIB (256 bits, CRC field inverted as check_CRC_bits leaves it) with
+// its CRC verdict goes to a raw callback as well.
+// The reference runs the decoding on its own thread behind a 3-slot queue and stop()
+// ends that thread; here decoding happens in the caller's thread (the GPU is the
+// parallel part) and after stop() process_ficBlock drops its input.
 class ficHandler {
 public:
     using fib_cb = std::function<void(const uint8_t *fib /*256 bits*/, bool crc_ok, int16_t ficno)>;
+    struct signals {
+        std::function<void(bool)> show_ficCRC;
+        fib_processor::ensemble_cb nameofEnsemble;
+        fib_processor::service_cb addtoEnsemble;
+    };
+    explicit ficHandler(signals sig, int16_t bitsperBlock = 2 * DABGPU_K);
     explicit ficHandler(fib_cb cb, int16_t bitsperBlock = 2 * DABGPU_K);
     void process_ficBlock(int16_t *data, int16_t blkno);   // blkno 1..3
-    int16_t get_ficRatio() const;                           // % of FIBs with a good CRC
+    void clearEnsemble();
+    int16_t get_ficRatio() const;                           // % of FIBs with a good CRC (*)
+    uint8_t kindofService(const std::string &s);
+    void dataforDataService(const std::string &s, packetdata *d);
+    void dataforAudioService(const std::string &s, audiodata *d);
+    void stop();
+    void on_fib(fib_cb cb) { cb_ = std::move(cb); }
+    // (*) the reference's ficRatio is never updated in v0.997 (fic-handler.cpp:186-188)
+    // the database, for callers that want more than the reference's lookups (under the lock)
+    template <class F> auto with_fib_processor(F f) {
+        std::lock_guard<std::mutex> g(fibHandling_);
+        return f(fibProcessor_);
+    }
 private:
+    void init(int16_t bitsperBlock);
     fib_cb cb_;
+    signals sig_;
     std::vector<int16_t> ofdm_input_;
     int index_ = 0, ficno_ = 0;
     int good_ = 0, total_ = 0;
+    std::atomic<bool> running_{true};
+    std::mutex fibHandling_;
+    fib_processor fibProcessor_;
     devbuf in_, bits_, crc_;
 };
 
@@ -195,9 +227,11 @@ public:
     dabConcurrent(uint8_t dabModus, int16_t fragmentSize, int16_t bitRate, int16_t uepFlag, int16_t protLevel,
                   std::unique_ptr<dabProcessor> processor);
     int32_t process(int16_t *v, int16_t cnt) override;
+    void setFiles(FILE *mp2, FILE *mp4) override;   // dab-concurrent.cpp:196-200
     dabProcessor *processor() { return proc_.get(); }
 protected:
     bool deinterleave(const int16_t *v);       // false during the warm-up
+    uint8_t dabModus_;
     int16_t fragmentSize_, bitRate_;
     dabgpu_subch sub_;
     std::vector<int16_t> delay_;               // [16][fragmentSize] ring of past fragments
@@ -225,7 +259,10 @@ private:
 // CIF's slice [startAddr * 64, + Length * 64) to a dabConcurrent (audio: mp2Processor
 // for DAB, mp4Processor for DAB+ (ASCTy 077)) or an mscDatagroup (data).  The channel
 // set by set_audioChannel / set_dataChannel (any thread, under the lock) takes effect
-// at the next process_mscBlock.  The decoded output goes to the callbacks.
+// at the next process_mscBlock.  The decoded output goes to the callbacks; setFiles
+// (msc-handler.cpp:208-212) dumps the DAB audio's MPEG frames into the mp2 file instead
+// (see mp2Processor), and keeps both files for the channels selected later
+// (msc-handler.cpp:147-150).
 class mscHandler {
 public:
     struct outputs {
@@ -241,10 +278,12 @@ public:
     int16_t getType();
     void stop();
     void stopProcessing();
+    void setFiles(FILE *mp2, FILE *mp4);
     dabVirtual *handler() { return dabHandler_.get(); }
 private:
     std::mutex locker_;
     outputs out_;
+    FILE *mp2File_ = nullptr, *mp4File_ = nullptr;
     int16_t BitsperBlock_, numberofblocksperCIF_;
     std::vector<int16_t> cifVector_;
     std::unique_ptr<dabVirtual> dabHandler_;

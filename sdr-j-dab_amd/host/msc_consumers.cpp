@@ -1,6 +1,7 @@
 // msc_consumers.cpp -- see msc_consumers.h.
 #include "msc_consumers.h"
 
+#include <algorithm>
 #include <cstring>
 
 namespace dabgpu {
@@ -19,8 +20,8 @@ bool check_CRC_bits(uint8_t *in, int16_t size) {
 }
 
 // ---- mp2Processor ---------------------------------------------------------------
-mp2Processor::mp2Processor(int16_t bitRate, frame_cb cb)
-    : cb_(std::move(cb)), MP2framesize_(24 * bitRate), MP2frame_(2 * 24 * bitRate, 0) {}
+mp2Processor::mp2Processor(int16_t bitRate, frame_cb cb, FILE *mp2file)
+    : cb_(std::move(cb)), mp2File_(mp2file), MP2framesize_(24 * bitRate), MP2frame_(2 * 24 * bitRate, 0) {}
 
 void mp2Processor::addbit(uint8_t b, int16_t nm) {                  // mp2processor.cpp:619-629
     uint8_t byte = MP2frame_[nm / 8];
@@ -36,7 +37,10 @@ void mp2Processor::addtoFrame(uint8_t *v, int16_t amount) {         // mp2proces
             addbit(v[i], MP2bitCount_++);
             if (MP2bitCount_ >= lf) {
                 frames_++;
-                if (cb_) cb_(MP2frame_.data(), lf, baudRate_);
+                if (mp2File_ != nullptr)
+                    (void)std::fwrite(MP2frame_.data(), sizeof(uint8_t), (size_t)lf, mp2File_);   // :581-582
+                else if (cb_)
+                    cb_(MP2frame_.data(), lf, baudRate_);
                 MP2Header_OK_ = 0;
                 MP2headerCount_ = 0;
                 MP2bitCount_ = 0;
@@ -86,14 +90,19 @@ void packetAssembler::add(uint8_t *data, int16_t length) {
     while (true) {                                                     // handlePackets (:221-234)
         const int16_t pLength = (int16_t)((bits_n(data, 0, 2) + 1) * 24 * 8);
         if (length < pLength) return;
-        handlePacket(data);
+        handlePacket(data, length);
         length = (int16_t)(length - pLength);
         if (length < 2) return;
         data = &data[pLength];
     }
 }
 
-void packetAssembler::handlePacket(uint8_t *data) {                    // msc-datagroup.cpp:241-319
+// avail: bits of the CIF from this packet on.  The reference copies 8 * usefulLength
+// bits from bit 24 whatever the packet length (msc-datagroup.cpp:276-283): a CRC-good
+// packet whose useful length exceeds it reads on into the next packets, and past the
+// CIF's buffer at its end -- here the copy stops at the buffer's end (defined behaviour;
+// the same bits wherever the reference's read is defined).
+void packetAssembler::handlePacket(uint8_t *data, int avail) {          // msc-datagroup.cpp:241-319
     const int16_t packetLength = (int16_t)((bits_n(data, 0, 2) + 1) * 24);
     const int16_t firstLast = (int16_t)bits_n(data, 4, 2);
     const int16_t address = (int16_t)bits_n(data, 6, 10);
@@ -108,8 +117,9 @@ void packetAssembler::handlePacket(uint8_t *data) {                    // msc-da
     if (streamAddress_ != address) return;
     auto take = [&](bool append) {
         const size_t cur = append ? series_.size() : 0;
-        series_.resize(cur + 8 * (size_t)usefulLength);
-        for (int i = 0; i < 8 * usefulLength; i++) series_[cur + i] = data[24 + i];
+        const int n = std::max(0, std::min(8 * (int)usefulLength, avail - 24));
+        series_.resize(cur + (size_t)n);
+        for (int i = 0; i < n; i++) series_[cur + i] = data[24 + i];
     };
     auto deliver = [&]() {
         datagroups_++;

@@ -273,6 +273,73 @@ void make_superframe(Rng &rng, int rsdims, uint8_t *sf /*[120*rsdims]*/) {
     }
 }
 
+// one MPEG-1 layer II frame (24 ms at 48 kHz = 24 * bitRate bits): sync 0xFFF, ID 1,
+// layer II, no CRC, the bit-rate index, 48 kHz; payload bytes below 0x80, so runs of
+// ones stay shorter than the 12 a receiver syncs on (mp2processor.cpp:594-603)
+void make_mp2_frame(Rng &rng, int bitRate, uint8_t *info /*[24 * bitRate] bits*/) {
+    static const int rates[15] = {0, 32, 48, 56, 64, 80, 96, 112, 128, 160, 192, 224, 256, 320, 384};
+    int idx = 8;
+    for (int i = 1; i < 15; i++)
+        if (rates[i] == bitRate) idx = i;
+    const int nbytes = 3 * bitRate;
+    for (int b = 0; b < nbytes; b++) {
+        uint8_t v = (uint8_t)(rng.next() & 0x7F);
+        if (b == 0) v = 0xFF;
+        else if (b == 1) v = 0xFD;                       // sync tail, ID 1, layer II, no CRC
+        else if (b == 2) v = (uint8_t)((idx << 4) | 0x04);   // bit rate, 48 kHz, no padding
+        else if (b == 3) v = 0x04;
+        for (int k = 0; k < 8; k++) info[8 * b + k] = (uint8_t)((v >> (7 - k)) & 1);
+    }
+}
+
+// packet mode (EN 300 401 5.3.2): per CIF 3 * bitRate bytes of packets (24, 48, 72 or 96
+// bytes: length index, continuity, first/last, address, command, useful length, data,
+// CRC-16); the packets of address `addr` carry MSC data groups of random length, split
+// over packets, with padding packets (address 0) in between now and then
+struct PacketState {
+    std::vector<uint8_t> group;    // rest of the data group in flight
+    bool started = false;          // its first packet went out
+    int cont = 0;
+};
+void make_packet_cif(Rng &rng, PacketState &st, int bitRate, int addr, uint8_t *info) {
+    const int nbytes = 3 * bitRate;
+    std::vector<uint8_t> out(nbytes, 0);
+    int pos = 0;
+    while (pos + 24 <= nbytes) {
+        int li = (int)(rng.next() % 4);
+        while (pos + 24 * (li + 1) > nbytes) li--;
+        const int L = 24 * (li + 1), room = L - 5;
+        uint8_t *p = &out[pos];
+        std::memset(p, 0, L);
+        const bool padding = rng.next() % 8 == 0;
+        int fl = 0, useful = 0, a = 0;
+        if (!padding) {
+            if (st.group.empty()) {
+                st.group.resize(20 + rng.next() % 300);
+                for (auto &b : st.group) b = (uint8_t)rng.next();
+                st.started = false;
+            }
+            useful = std::min<int>(room, (int)st.group.size());
+            const bool first = !st.started, last = useful == (int)st.group.size();
+            fl = (first ? 2 : 0) | (last ? 1 : 0);
+            std::memcpy(p + 3, st.group.data(), useful);
+            st.group.erase(st.group.begin(), st.group.begin() + useful);
+            st.started = true;
+            a = addr;
+        }
+        p[0] = (uint8_t)((li << 6) | ((st.cont & 3) << 4) | (fl << 2) | ((a >> 8) & 3));
+        p[1] = (uint8_t)(a & 0xFF);
+        p[2] = (uint8_t)(useful & 0x7F);                  // command flag 0
+        st.cont++;
+        const uint16_t c = (uint16_t)~crc_ccitt(p, L - 2);
+        p[L - 2] = (uint8_t)(c >> 8);
+        p[L - 1] = (uint8_t)(c & 0xFF);
+        pos += L;
+    }
+    for (int b = 0; b < nbytes; b++)
+        for (int k = 0; k < 8; k++) info[8 * b + k] = (uint8_t)((out[b] >> (7 - k)) & 1);
+}
+
 }  // namespace
 
 extern "C" {
@@ -370,7 +437,16 @@ static void make_fig_fib(const dabsynth_cfg *cfg, int64_t n, uint8_t *fib) {
         }
         w.put(0, 3), w.put(6, 5), w.put(0, 3), w.put(2, 5);
         w.put(0xC000 + i, 16), w.put(0, 1), w.put(0, 3), w.put(1, 4);
-        w.put(0, 2), w.put(sc.dabplus ? 63 : 0, 6), w.put(i, 6), w.put(1, 1), w.put(0, 1);
+        if (!sc.dabplus && sc.content == DABSYNTH_PACKET) {
+            // packet-mode component (TMid 3, SCId 0x400 + i), then FIG 0/3: SCId -> DG flag 0,
+            // DSCTy 60 (MOT), sub-channel i, packet address 0x100 + i
+            w.put(3, 2), w.put(0x400 + i, 12), w.put(1, 1), w.put(0, 1);
+            w.put(0, 3), w.put(6, 5), w.put(0, 3), w.put(3, 5);
+            w.put(0x400 + i, 12), w.put(0, 3), w.put(0, 1), w.put(0, 1), w.put(0, 1);
+            w.put(60, 6), w.put(i, 6), w.put(0x100 + i, 10);
+        } else {
+            w.put(0, 2), w.put(sc.dabplus ? 63 : 0, 6), w.put(i, 6), w.put(1, 1), w.put(0, 1);
+        }
     }
     for (int k = (w.pos + 7) >> 3; k < 30; k++) bytes[k] = 0xFF;    // end marker / padding
     const uint16_t c = (uint16_t)~crc_ccitt(bytes, 30);
@@ -414,13 +490,14 @@ static int gen_core(const dabsynth_cfg *cfg, uint64_t seed, int P, float *iq, ui
     const int e0 = cyc ? 0 : -19, NE = 4 * F - e0, NC = 4 * F;
     std::vector<std::vector<uint8_t>> enc_frag(NS);      // punctured bits per (e, s)
     std::vector<int> frag_len(NS);
+    std::vector<PacketState> pst(NS);
     for (int s = 0; s < NS; s++) {
         const dabsynth_subch &sc = cfg->subch[s];
         int nb = 24 * sc.bitRate;
         if (cyc && sc.dabplus && NC % 5) return -3;      // superframes must tile the period
         frag_len[s] = sc.length * 64;
         enc_frag[s].assign((size_t)NE * frag_len[s], 0);
-        std::vector<uint8_t> info(nb), mother(4 * (nb + 6)), punct(frag_len[s] + 64);
+        std::vector<uint8_t> info(nb), mother(4 * (nb + 6)), punct(std::max<size_t>(frag_len[s], mother.size()));
         int rsdims = sc.bitRate / 8;
         std::vector<uint8_t> sf(120 * std::max(rsdims, 1));
         // dabplus = 1 + k: the superframe grid is shifted by k CIFs (k = 1..4 makes the
@@ -436,6 +513,10 @@ static int gen_core(const dabsynth_cfg *cfg, uint64_t seed, int P, float *iq, ui
                     for (int b = 0; b < 8; b++) info[8 * byte + b] = (uint8_t)((v >> (7 - b)) & 1);
                     sf_pos = (sf_pos + 1) % (120 * rsdims);
                 }
+            } else if (sc.content == DABSYNTH_MP2) {
+                make_mp2_frame(rng, sc.bitRate, info.data());
+            } else if (sc.content == DABSYNTH_PACKET) {
+                make_packet_cif(rng, pst[s], sc.bitRate, 0x100 + s, info.data());
             } else {
                 for (int i = 0; i < nb; i++) info[i] = rng.bit();
             }

@@ -28,7 +28,14 @@ typedef struct {
     int16_t protLevel;   /* UEP level 1..5, or EEP 0100|lvl (A) / 0200|lvl (B) */
     int16_t uep;         /* 1 = UEP (uepFlag 0 in the reference), 0 = EEP */
     int16_t dabplus;     /* 1+k: DAB+ superframe stream (valid RS/fire code/AU CRCs), grid shifted by k CIFs */
+    int16_t content;     /* with dabplus 0: 0 random bits; DABSYNTH_MP2: one MPEG-1 layer II frame per
+                            CIF (48 kHz, sync + header, payload bytes < 0x80 so only headers carry
+                            12 ones in a row); DABSYNTH_PACKET: packet mode, 24..96-byte packets with
+                            CRCs carrying MSC data groups (address 0x100 + subchannel index, some
+                            padding packets), announced as DSCTy 60 by FIG 0/2 (TMid 3) + FIG 0/3 */
 } dabsynth_subch;
+#define DABSYNTH_MP2 2
+#define DABSYNTH_PACKET 3
 
 typedef struct {
     int32_t n_frames;    /* frames after the pre-roll */

@@ -270,7 +270,7 @@ class Datagroups:
         return r
 
     def add(self, bits):
-        data = list(bits)
+        data = [int(x) for x in bits]
         if self.dscty == 5 and self.dgflag:
             pl = (self._get(data, 0, 2) + 1) * 24
             seg = data[:pl * 8]

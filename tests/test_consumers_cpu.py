@@ -116,3 +116,33 @@ def test_packet_datagroups_match_reference():
     assert len(o.groups) >= 4 and o.crc_errors >= 1
     assert got == o.groups
     assert l.cw_pa_crc_errors(h) == o.crc_errors
+
+
+def test_transmitter_mp2_and_packet_subchannels():
+    """The transmitter's MPEG layer II and packet-mode subchannels (dabsynth content
+    MP2 / PACKET): the oracle's consumers find one frame per CIF and whole data groups
+    with good CRCs in the transmitted bits, and the product's consumers agree."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sdr-j-dab_amd"))
+    from dabamd.synth import Ensemble, MP2, PACKET
+    sub = [(0, 96, 128, 0o103, 0, 0, MP2), (96, 24, 32, 0o103, 0, 0, PACKET)]
+    ens = Ensemble(6, subch=sub)
+    g = ens.generate(5)
+    l = _lib()
+    m, hm = orc.MP2(128), l.cw_mp2_new(128)
+    d, hd = orc.Datagroups(60, 0), l.cw_pa_new(60, 0)
+    for c in range(16, 24):
+        fb = np.ascontiguousarray(g["msc"][c, 0, :24 * 128])
+        pb = np.ascontiguousarray(g["msc"][c, 1, :24 * 32])
+        assert bytes(np.packbits(fb)[:4]) == bytes([0xFF, 0xFD, 0x84, 0x04])
+        m.add(fb)
+        fc, pc = fb.copy(), pb.copy()                  # (the consumers invert CRC bits in place)
+        l.cw_mp2_add(hm, orc.P(fc), len(fc))
+        d.add(pb)
+        l.cw_pa_add(hd, orc.P(pc), len(pc))
+    assert len(m.frames) == 8 and all(r == 48000 for _, r in m.frames)
+    assert [f for f, _ in m.frames] == [bytes(np.packbits(g["msc"][c, 0, :24 * 128])) for c in range(16, 24)]
+    assert _items(l, hm) == m.frames
+    assert d.crc_errors == 0 and len(d.groups) >= 2
+    assert [list(x) for x, _ in _items(l, hd)] == d.groups
+    assert l.cw_pa_crc_errors(hd) == 0
