@@ -806,6 +806,10 @@ struct dabgpu_pipe {
     int32_t *h_ncif = nullptr, *h_slots = nullptr;
     hipEvent_t ev_copy[2] = {nullptr, nullptr};
     bool copy_rec[2] = {false, false};
+    // the back-end streams' own error words (the front end's is the context's): the
+    // Viterbi jobs of run r set berr_d[r & 1], which the back end publishes into
+    // h_berr[r & 1] (and clears) as its last step; read once ev_back[r & 1] completed
+    int32_t *berr_d = nullptr, *h_berr = nullptr;
     // speculative back end (dabgpu_pipe_run): queued behind the first front pass
     bool speculate = true;                      // env DABGPU_NO_SPECULATE=1: off (A/B)
     int64_t front_launches = 0, spec_runs = 0, spec_hits = 0;
@@ -867,6 +871,23 @@ static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
     hipError_t r = hipEventRecord(p->ev_pool[p->ev_rec.back().second + 1], st);
     if (r == hipSuccess && p->profiling == 3) r = hipDeviceSynchronize();
     return r;
+}
+
+// errors the back-end streams' kernels raised (refused out-of-bounds Viterbi sources):
+// read for every back end known complete -- after a sync (wait) or by a non-blocking
+// query -- and reported once
+static int back_errors(dabgpu_pipe *p, bool wait) {
+    for (int par = 0; par < 2; par++) {
+        if (!p->back_rec[par]) continue;
+        if (!wait && hipEventQuery(p->ev_back[par]) != hipSuccess) continue;
+        const int32_t e = *(volatile int32_t *)&p->h_berr[par];
+        if (e) {
+            p->h_berr[par] = 0;
+            return fail(DABGPU_E_BOUNDS, "kernel refused out-of-bounds work on back-end stream %d:%s", par,
+                        (e & KERR_VITERBI) ? " viterbi source" : " (unknown)");
+        }
+    }
+    return 0;
 }
 
 namespace {
@@ -945,8 +966,12 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
                 hipHostMalloc((void **)&p->h_snr, sizeof(int16_t) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_cif0, sizeof(int64_t) * p->S * 2, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_ncif, sizeof(int32_t) * p->S * 2, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&p->h_slots, sizeof(int32_t) * SF * 2, hipHostMallocDefault) != hipSuccess))
+                hipHostMalloc((void **)&p->h_slots, sizeof(int32_t) * SF * 2, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_berr, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess))
         rc = fail(DABGPU_E_NOMEM, "pipe pinned staging");
+    A((void **)&p->berr_d, sizeof(int32_t) * 2);
+    if (!rc && (hipMemset(p->berr_d, 0, sizeof(int32_t) * 2) != hipSuccess)) rc = fail(DABGPU_E_HIP, "pipe error words");
+    if (!rc) p->h_berr[0] = p->h_berr[1] = 0;
     if (const char *e = getenv("DABGPU_NO_SPECULATE")) p->speculate = !(e[0] == '1');
     A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
     A((void **)&p->cif0_d, sizeof(int64_t) * p->S * 2);
@@ -1028,11 +1053,11 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
     for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_cif0,
-                    (void *)p->h_ncif, (void *)p->h_slots})
+                    (void *)p->h_ncif, (void *)p->h_slots, (void *)p->h_berr})
         if (h) (void)hipHostFree(h);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->inv_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
-                    (void *)p->cif0_d, (void *)p->ncif_d,
+                    (void *)p->cif0_d, (void *)p->ncif_d, (void *)p->berr_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d,
                     (void *)p->dp_cand_d})
         if (x) (void)hipFree(x);
@@ -1388,6 +1413,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     const int S = p->S, F = p->F;
     const bool do_msc = msc_bits && p->NSUB > 0;
     if (do_msc && msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
+    if (int rc = back_errors(p, false)) return rc;
     p->last_frames.assign((size_t)S * F, dabgpu_frame());
     p->last_si.assign((size_t)S * F, 0);
     p->last_info.assign((size_t)S * F, dabgpu_frame_info());
@@ -1435,7 +1461,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             JF.n_cw = 4 * S * F;
             JF.src = p->ring;
             JF.src_len = (int64_t)S * p->R * FRAME_SOFT;
-            JF.err = c->err;
+            JF.err = p->berr_d + par;
             JF.slots = slots_d;
             JF.prof = (const Profile *)p->ficprof_d;
             JF.inv = c->fic_inv;
@@ -1452,7 +1478,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             JM.n_cw = S * 4 * F * p->NSUB;
             JM.src = p->ring;
             JM.src_len = (int64_t)S * p->R * FRAME_SOFT;
-            JM.err = c->err;
+            JM.err = p->berr_d + par;
             JM.prof = p->prof_d;
             JM.inv = p->inv_d;
             JM.nsub = p->NSUB;
@@ -1522,7 +1548,20 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         }
     }
     bool spec_sent = false;
+    size_t spec_rec0 = 0, spec_rec1 = 0;         // profiling records of the speculative enqueue
     int passes = 0;
+    // an error after the speculative back end was queued: it still writes the caller's
+    // outputs and reads ring slots, so it is tracked like a completed run's back end
+    // (the next run's demod waits for it) and finished before the error returns
+    auto bail = [&](int rc) -> int {
+        if (spec_sent) {
+            (void)launch_take_error(bs, p->berr_d + par, p->h_berr + par);
+            (void)hipEventRecord(p->ev_back[par], bs);
+            p->back_rec[par] = true;
+            (void)hipStreamSynchronize(bs);
+        }
+        return rc;
+    };
     // ofdmProcessor::run per stream: speculative front-end passes commit frames; a
     // stream that loses sync (or was never synchronised) searches the next null
     // symbol from where it is and continues (goto notSynced, ofdm-processor.cpp:354-357).
@@ -1532,16 +1571,19 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         for (int s = 0; s < S; s++)
             if (!cur[s].synced && done[s] < F) who.push_back(s);
         int found = 0;
-        if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) return rc;
+        if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) return bail(rc);
         bool progress = false, lost = false;
         std::function<int()> after;
         if (spec && it == 0 && found == 0)
             after = [&]() -> int {
                 spec_sent = true;
-                return enqueue_back(pred, pred_slot);
+                spec_rec0 = p->ev_rec.size();
+                const int rc = enqueue_back(pred, pred_slot);
+                spec_rec1 = p->ev_rec.size();
+                return rc;
             };
         const int64_t launches_before = p->front_launches;
-        if (int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost, after)) return rc;
+        if (int rc = pipe_front_pass(p, iq, stride, n_avail, done, cur, progress, lost, after)) return bail(rc);
         if (p->front_launches != launches_before) passes++;
         if (!progress && !lost && !found) break;
     }
@@ -1556,8 +1598,12 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     bool hit = spec_sent && passes == 1 && done == pred && slot == pred_slot;
     p->spec_runs += spec_sent ? 1 : 0;
     p->spec_hits += hit ? 1 : 0;
-    if (!hit)
-        if (int rc = enqueue_back(done, slot)) return rc;
+    if (!hit) {
+        // the speculative decode is overwritten: its stage times are not this run's
+        for (size_t i = spec_rec0; i < spec_rec1; i++) p->ev_rec[i].first = -1;
+        if (int rc = enqueue_back(done, slot)) return bail(rc);
+    }
+    HIPCHK(launch_take_error(bs, p->berr_d + par, p->h_berr + par));
     HIPCHK(hipEventRecord(p->ev_back[par], bs));
     p->back_rec[par] = true;
     p->run_idx++;
@@ -1589,6 +1635,7 @@ int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
     for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
     for (int k = 0; k < DABGPU_NSTAGE; k++) { p->stage_ms[k] = 0.0f; p->stage_n[k] = 0; }
     for (auto &r : p->ev_rec) {
+        if (r.first < 0) continue;              // discarded (a missed speculation)
         float t = 0.0f;
         HIPCHK(hipEventElapsedTime(&t, p->ev_pool[r.second], p->ev_pool[r.second + 1]));
         p->stage_ms[r.first] += t;
@@ -1605,6 +1652,7 @@ int dabgpu_pipe_sync(dabgpu_pipe *p) {
     if (!p) return fail(DABGPU_E_ARG, "null pipe");
     HIPCHK(hipStreamSynchronize(p->c->stream));
     for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
+    if (int rc = back_errors(p, true)) return rc;
     return kernel_errors(p->c);
 }
 

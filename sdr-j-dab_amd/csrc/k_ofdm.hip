@@ -290,7 +290,16 @@ __global__ void k_front_publish(const float2 *__restrict__ part, int nchunks, in
     h_snr[f] = snr_d[f];
 }
 
+// a back-end stream's error word, taken (cleared) and or-ed into its pinned host copy
+__global__ void k_take_error(int32_t *err, int32_t *h_err) {
+    if (threadIdx.x == 0) *h_err |= atomicExch(err, 0);
+}
+
 // ---- launchers -----------------------------------------------------------
+hipError_t launch_take_error(hipStream_t st, int32_t *err, int32_t *h_err) {
+    hipLaunchKernelGGL(k_take_error, dim3(1), dim3(64), 0, st, err, h_err);
+    return hipGetLastError();
+}
 hipError_t launch_front_publish(hipStream_t st, const float *part, int nchunks, int n, float *fc_d, float *h_fc,
                                 const int32_t *si_d, int32_t *h_si, const int16_t *snr_d, int16_t *h_snr,
                                 int32_t *err, int32_t *h_err) {
