@@ -167,6 +167,7 @@ hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr,
 hipError_t launch_nco_eval(hipStream_t st, const OfdmTables &T, int32_t first, int32_t n, float2 *out);
 hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmTables &T, float *spec, int16_t *ibits);
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
+hipError_t launch_take_error(hipStream_t st, int32_t *err, int32_t *h_err);
 hipError_t launch_front_publish(hipStream_t st, const float *part, int nchunks, int n, float *fc_d, float *h_fc,
                                 const int32_t *si_d, int32_t *h_si, const int16_t *snr_d, int16_t *h_snr,
                                 int32_t *err, int32_t *h_err);
