@@ -125,7 +125,12 @@ def lib() -> C.CDLL:
             "dabgpu_pipe_timing": ([vp, vp, vp], i32),
         }
         for name, (args, res) in sig.items():
-            f = getattr(l, name)
+            try:
+                f = getattr(l, name)
+            except AttributeError:
+                if "DABGPU_LIB" in os.environ:           # an older A/B build (tools/): calls to it raise
+                    continue
+                raise
             f.argtypes, f.restype = args, res
         _lib = l
     return _lib
@@ -581,6 +586,7 @@ class Pipeline:
         return list(fr), si.reshape(self.S, self.F)
 
     def softbits(self) -> np.ndarray:
+        """the soft-bit ring of the last run as [stream][slot][75][3072] ibits rows"""
         p, r = C.c_void_p(), C.c_int32()
         _chk(lib().dabgpu_pipe_softbits(self.h, C.byref(p), C.byref(r)), "softbits")
         n = self.S * r.value * NSYM * SYMBITS
