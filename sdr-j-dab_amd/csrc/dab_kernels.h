@@ -64,11 +64,6 @@ struct AcqResult {
 // contiguous: dec[((row / 64 * dec_nch + chunk) * 64 + row % 64) * 64 + lane]
 // (dec_word_index); rows padded to a whole block of 64
 constexpr int DEC_WORD_STEPS = 30;
-// the tile loader's inverse depuncturing table in pairs (one 4-byte load gives two rounds'
-// mother-code positions): A/B hook, host and kernels compiled alike
-#ifndef ACS_INV_PAIRS
-#define ACS_INV_PAIRS 0                    // 1 measured 2 % slower in k_acs2 (profiles/r02_acs_ab.txt)
-#endif
 inline __host__ __device__ int64_t dec_rows(int n_cw) { return ((int64_t)n_cw + 63) / 64 * 64; }
 inline __host__ __device__ int32_t dec_chunks(int nbits) { return (nbits + 6 + DEC_WORD_STEPS - 1) / DEC_WORD_STEPS; }
 inline __host__ __device__ int64_t dec_bytes(int n_cw, int nbits) {
@@ -125,8 +120,7 @@ struct VitJob {
     const uint32_t *prbs_words;     // PRBS packed 32 bits per word, bit i = prbs[32w+i]
     const uint8_t *valid;           // optional per-codeword flag: 0 = skip
     // SRC_MSC / SRC_FIC: inverse depuncturing tables, Profile::frag uint16 mother-code
-    // positions per profile at Profile::inv_off (make_inv); null: step-major loader.
-    // ACS_INV_PAIRS: 2 * frag uint16, entry i = {position of input i, of input i + 64}
+    // positions per profile at Profile::inv_off (make_inv); null: step-major loader
     const uint16_t *inv;
 };
 

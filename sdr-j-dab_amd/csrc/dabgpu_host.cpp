@@ -290,14 +290,7 @@ std::vector<uint16_t> make_inv(const Profile &P) {
         }
         if (keep) inv.push_back((uint16_t)q);
     }
-    if (!ACS_INV_PAIRS) return inv;
-    // pairs {input i, input i + 64}: the loader's rounds k and k + 1 in one 4-byte load
-    std::vector<uint16_t> pr(2 * inv.size());
-    for (size_t i = 0; i < inv.size(); i++) {
-        pr[2 * i] = inv[i];
-        pr[2 * i + 1] = i + 64 < inv.size() ? inv[i + 64] : 0;
-    }
-    return pr;
+    return inv;
 }
 
 }  // namespace

@@ -379,12 +379,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
             mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
             float mx, sm;
-#ifdef DEMOD_FAKE_SYNC  // A/B measurement only (tools/build_variant.sh): the frame's own block0
-            const int32_t si = (int32_t)(fr.block0 - fr.window) + (a[0].x == 12345.0f ? 1 : 0);
-            mx = sm = 0.0f;
-#else
             const int32_t si = prs_corr_wg(a, ex, tw, t, T.ref, aux.level, red, mx, sm);
-#endif
             if (ch == 0 && t == 0) {
                 aux.si[fi] = si;
                 if (aux.maxv) aux.maxv[fi] = mx;
@@ -416,11 +411,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         {
             const int b0 = bin0_of(t);
             auto slot = [&](int k3) -> uint32_t {
-#ifdef DEMOD_AB_NOPERM      // A/B timing only: bin-order LDS stage (no de-interleave scatter)
-                const int c = k3 < 6 ? k3 * DT + t : -1;
-#else
                 const int c = T.carrier_of_bin[b0 + 64 * k3];
-#endif
                 return (uint32_t)(c >= 0 ? c : K + t) * 4u;
             };
 #pragma unroll
@@ -523,11 +514,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 // ab1 = |re| + |im| (ofdm-decoder.cpp:185-189)
                 const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                 int ir, ii;
-#ifdef DEMOD_AB_FASTSOFT    // A/B timing only (tools/build_variant.sh): no exactness check
-                { const float mm = __builtin_amdgcn_rcpf(ab1) * -127.0f; ir = (int)(r1.x * mm); ii = (int)(r1.y * mm); }
-#else
                 risky |= (uint32_t)soft_fast(r1, ab1, ir, ii) << k;
-#endif
                 const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
                 *(uint32_t *)((char *)st + addr) = __builtin_amdgcn_perm((uint32_t)ii, (uint32_t)ir, 0x05040100u);
             }

@@ -301,40 +301,27 @@ __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4])
 // sum first, then a bank-masked DPP add over the lanes that take their partner's
 // metric; M = 32 goes through one permlane swap (a copy, a hazard wait and a
 // quarter-rate swap), M = 16 reads P and Q through the LDS crossbar (two ds_swizzle
-// within 32 lanes), which leaves that step's VALU to the two adds.  ACS_LDS_MOVES bit 1
-// moves M = 32 to the crossbar (ds_bpermute across the halves; bpa / bpb = byte
-// addresses of lane & 31 and lane | 32): 8 % fewer cycles per step in the ACS alone
-// (tools/acs_core.hip, profiles/r02_acs_core.txt) but slower in the kernel, whose tile
-// loader also lives on the LDS; M = 16 alone measured 1.5 % faster (r02_acs_ab.txt).
+// within 32 lanes), which leaves that step's VALU to the two adds.  Measured (round 2,
+// profiles/r02_acs_core.txt, r02_acs_ab.txt): the crossbar for M = 32 is 8 % faster in the
+// ACS alone but slower in the kernel, whose tile loader also lives on the LDS; for M = 16
+// alone 1.5 % faster; for M = 4 / 8 no gain.
 // DPP hazard: a DPP source written by the previous VALU instruction needs two wait
 // states -- only the first quad_perm add follows the metric update directly (s_nop 1);
 // the bank-masked adds come after the two plain adds that also read x.
-#ifndef ACS_LDS_MOVES
-#define ACS_LDS_MOVES 1            // A/B hook (tools/build_variant.sh): bit 0 = M = 16 through
-                                   // the LDS crossbar, bit 1 = M = 32, bit 2 = M = 8, bit 3 = M = 4
-#endif
 #define DPP_ADD(ctl) "v_add_u32_dpp %0, %1, %2 " ctl
 #define DPP_ADD_NOP(ctl) "s_nop 1\n\tv_add_u32_dpp %0, %1, %2 " ctl
 template <int M>
-__device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint32_t &A, uint32_t &B, int bpa,
-                                     int bpb) {
+__device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint32_t &A, uint32_t &B) {
     if constexpr (M == 1) {
         asm(DPP_ADD_NOP("quad_perm:[0,0,2,2] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
         asm(DPP_ADD("quad_perm:[1,1,3,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 2) {
         asm(DPP_ADD_NOP("quad_perm:[0,1,0,1] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
         asm(DPP_ADD("quad_perm:[2,3,2,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
-    } else if constexpr (M == 16 && (ACS_LDS_MOVES & 1)) {
+    } else if constexpr (M == 16) {
         // swizzle bit mode: lane' = (lane & and) | or within 32 lanes
         A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x0F) + ta;              // lane & ~16
         B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 5)) + tb; // lane | 16
-    } else if constexpr (M == 32 && (ACS_LDS_MOVES & 2)) {
-        A = (uint32_t)__builtin_amdgcn_ds_bpermute(bpa, (int)x) + ta;
-        B = (uint32_t)__builtin_amdgcn_ds_bpermute(bpb, (int)x) + tb;
-    } else if constexpr ((M == 4 && (ACS_LDS_MOVES & 8)) || (M == 8 && (ACS_LDS_MOVES & 4))) {
-        // swizzle bit mode: P = lane & ~M, Q = lane | M
-        A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F & ~M) + ta;
-        B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (M << 5)) + tb;
     } else if constexpr (M == 4) {
         // upper lanes (banks 1,3 of each row) take lane-4 as P; lower lanes (banks 0,2) lane+4 as Q
         // (one asm block: the two plain adds are the wait states before the DPP reads x)
@@ -347,10 +334,6 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
             "v_add_u32_dpp %0, %2, %3 row_shr:8 row_mask:0xf bank_mask:0xc\n\t"
             "v_add_u32_dpp %1, %2, %4 row_shl:8 row_mask:0xf bank_mask:0x3"
             : "=&v"(A), "=&v"(B) : "v"(x), "v"(ta), "v"(tb));
-    } else if constexpr (M == 16) {
-        auto r = __builtin_amdgcn_permlane16_swap(x, x, false, false);   // odd rows <-> even rows
-        A = r[0] + ta;
-        B = r[1] + tb;
     } else {
         static_assert(M == 32, "xor distance");
         auto r = __builtin_amdgcn_permlane32_swap(x, x, false, false);
@@ -361,12 +344,6 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
 #undef DPP_ADD
 #undef DPP_ADD_NOP
 
-// w = (w >> 1) with the bits of e under mask m inserted (one v_lshrrev + one v_bfi)
-__device__ __forceinline__ uint32_t bits_in(uint32_t m, uint32_t w, uint32_t e) {
-    uint32_t r;
-    asm("v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "s"(m), "v"(e), "v"(w >> 1));
-    return r;
-}
 // w with the bits of e under mask m (one v_bfi)
 __device__ __forceinline__ uint32_t bits_put(uint32_t m, uint32_t w, uint32_t e) {
     uint32_t r;
@@ -374,26 +351,15 @@ __device__ __forceinline__ uint32_t bits_put(uint32_t m, uint32_t w, uint32_t e)
     return r;
 }
 // Decision bits in a stored word.  v_bfi and v_perm issue at half rate on gfx950
-// (profiles/r02_valu_rate.txt), the shift at full rate.
-//   ACS_DEC_PAIRS 0: shift-in per step (sign bits 15 / 31 of d), dpos(k) = k.
-//   ACS_DEC_PAIRS 1: per pair of steps (2p, 2p+1) one v_perm joins the bytes holding the
-//     four sign bits (bit 7 of {d_2p.b1, d_2p.b3, d_2p+1.b1, d_2p+1.b3}) and one shift +
-//     v_bfi moves them into bit 7 of the four bytes of a collector.
-//   ACS_DEC_PAIRS 2 (default): the v_perm selectors 8..11 (a byte of copies of bit 15 /
-//     31 of either source) turn the four decisions into four 0x00 / 0xFF bytes at once,
-//     and one v_bfi with the mask 0x01010101 << (p & 7) drops them into bit p & 7 of the
-//     collector's bytes -- no shift: 1 instead of 1.5 instructions per step.
+// (profiles/r02_valu_rate.txt): per pair of steps (2p, 2p+1) the v_perm selectors 8..11
+// (a byte of copies of bit 15 / 31 of either source) turn the four decisions into four
+// 0x00 / 0xFF bytes at once, and one v_bfi with the mask 0x01010101 << (p & 7) drops them
+// into bit p & 7 of a collector's bytes -- 1 instruction per step (round 2 measured a
+// shift-in per step and a v_perm + shift + v_bfi per pair slower, r02_acs_ab.txt).
 // Collector a takes pairs 0..7, b pairs 8..14; the stored word of codeword 0 is
 // {a.b0, a.b2, b.b0, b.b2}, of codeword 1 {a.b1, a.b3, b.b1, b.b3}.
 // dpos(k) = bit of trellis step k (k < 30) of a chunk in its word.
-#ifndef ACS_DEC_PAIRS
-#define ACS_DEC_PAIRS 2            // A/B hook
-#endif
-__host__ __device__ constexpr int dpos(int k) {
-    return ACS_DEC_PAIRS == 0 ? k
-         : k < 16             ? 8 * (k & 1) + (k >> 1)
-                              : 16 + 8 * (k & 1) + (k >> 1) - (ACS_DEC_PAIRS == 1 ? 7 : 8);
-}
+__host__ __device__ constexpr int dpos(int k) { return k < 16 ? 8 * (k & 1) + (k >> 1) : 8 + 8 * (k & 1) + (k >> 1); }
 
 // subtract a common offset from all states of each codeword (see header)
 __device__ __forceinline__ uint32_t renorm(uint32_t x) {
@@ -415,14 +381,12 @@ __device__ __forceinline__ uint32_t renorm(uint32_t x) {
 template <int NP, bool FULL>
 __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
                                             uint32_t (&cw)[2 * NP]) {
-    static_assert(WS == 30, "two 15-step half-words per decision word");
+    static_assert(WS == 30, "two collectors of 8 and 7 step pairs per decision word");
     // the 6 per-phase row addresses once per word: each step's read is then one
     // ds_read_b64 at an immediate offset
     const uint32_t *rp[6];
 #pragma unroll
     for (int r = 0; r < 6; r++) rp[r] = bm + row[r];
-    const int lane = threadIdx.x;
-    const int bpa = 4 * (lane & 31), bpb = 4 * (lane | 32);
     uint32_t w[NP], w0[NP], dp[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) w[p] = dp[p] = 0;
@@ -435,7 +399,7 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (
                 constexpr int p = decltype(pc)::value;
                 const uint2 t = *(const uint2 *)(rp[rho] + p * 8 * BRS + 2 * j);
                 uint32_t A, B;
-                cand<(32 >> rho)>(x[p], t.x, t.y, A, B, bpa, bpb);
+                cand<(32 >> rho)>(x[p], t.x, t.y, A, B);
                 d[p] = as_u32(as_pk(B) - as_pk(A));
                 x[p] = as_u32(__builtin_elementwise_min(as_pk(A), as_pk(B)));
             });
@@ -445,34 +409,21 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (
         }
 #pragma unroll
         for (int p = 0; p < NP; p++) {
-            if constexpr (!ACS_DEC_PAIRS) {
-                w[p] = bits_in(0x80008000u, w[p], d[p]);
-            } else if constexpr ((j & 1) == 0) {
-                dp[p] = d[p];
-            } else if constexpr (ACS_DEC_PAIRS == 1) {
-                w[p] = bits_in(0x80808080u, w[p], __builtin_amdgcn_perm(d[p], dp[p], 0x07050301u));
-            } else {
-                w[p] = bits_put(0x01010101u << ((j >> 1) & 7), w[p], __builtin_amdgcn_perm(d[p], dp[p], 0x0B0A0908u));
-            }
+            if constexpr ((j & 1) == 0) dp[p] = d[p];
+            else w[p] = bits_put(0x01010101u << ((j >> 1) & 7), w[p], __builtin_amdgcn_perm(d[p], dp[p], 0x0B0A0908u));
         }
-        if constexpr (j == (ACS_DEC_PAIRS ? 15 : WS / 2 - 1)) {
+        if constexpr (j == 15) {
 #pragma unroll
             for (int p = 0; p < NP; p++) {
                 w0[p] = w[p];
-                if constexpr (ACS_DEC_PAIRS) w[p] = 0;
+                w[p] = 0;
             }
         }
     });
 #pragma unroll
     for (int p = 0; p < NP; p++) {
-        if constexpr (ACS_DEC_PAIRS) {
-            cw[2 * p] = __builtin_amdgcn_perm(w[p], w0[p], 0x06040200u);
-            cw[2 * p + 1] = __builtin_amdgcn_perm(w[p], w0[p], 0x07050301u);
-        } else {
-            // half-word h holds step 15h + k at bit k + 1 (codeword 0) and k + 17 (codeword 1)
-            cw[2 * p] = ((w0[p] >> 1) & 0x7FFFu) | ((w[p] << 14) & 0x3FFF8000u);
-            cw[2 * p + 1] = ((w0[p] >> 17) & 0x7FFFu) | ((w[p] >> 2) & 0x3FFF8000u);
-        }
+        cw[2 * p] = __builtin_amdgcn_perm(w[p], w0[p], 0x06040200u);
+        cw[2 * p + 1] = __builtin_amdgcn_perm(w[p], w0[p], 0x07050301u);
     }
 #pragma unroll
     for (int p = 0; p < NP; p++) x[p] = renorm(x[p]);
@@ -488,9 +439,6 @@ __device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&ro
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++)
         if (rb[k] >= 0)
-#ifdef ACS_AB_NODEC          // A/B timing only: decisions not written (cost of the decision traffic)
-            if ((cw[k] ^ (uint32_t)o) == 0xDEADBEEFu)
-#endif
             __builtin_amdgcn_raw_buffer_store_b32(cw[k], drs, 4 * lane, (int)(4 * (rb[k] + o)), 0);
 }
 
@@ -539,7 +487,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
     const int frag = __builtin_amdgcn_readfirstlane(J.prof[prof].frag);
     const int ioff = __builtin_amdgcn_readfirstlane(J.prof[prof].inv_off);
     const __amdgpu_buffer_rsrc_t rinv =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, (ACS_INV_PAIRS ? 4 : 2) * frag, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, 2 * frag, 0x00020000);
     u16x2 vab[IN_K];                       // the pair's inputs, packed
     uint32_t vm[IN_K];                     // their mother-code positions
     int I0 = 0, I1 = 0;
@@ -550,19 +498,13 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         int2 ro;
         if constexpr (KIND == SRC_MSC) ro = ro2[i & 15];
         else ro = make_int2(c[0].valid ? 0 : RO_EMPTY, c[1].valid ? 0 : RO_EMPTY);
-        const int oa = ro.x + 2 * i, ob = ro.y + 2 * i, oi = (ACS_INV_PAIRS ? 4 : 2) * i;
+        const int oa = ro.x + 2 * i, ob = ro.y + 2 * i, oi = 2 * i;
 #pragma unroll
         for (int k = 0; k < IN_K; k++) {
             if (64 * k < I1 - I0) {
                 vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
                 vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);
-                if constexpr (!ACS_INV_PAIRS) {
-                    vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
-                } else if ((k & 1) == 0) {                // rounds k, k + 1 (unrolled: k constant)
-                    const uint32_t v = __builtin_amdgcn_raw_buffer_load_b32(rinv, oi, 512 * (k >> 1), 0);   // entry i + 128 * (k / 2)
-                    vm[k] = v & 0xFFFFu;
-                    if (k + 1 < IN_K) vm[k + 1] = v >> 16;
-                }
+                vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
             }
         }
     };
@@ -740,9 +682,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     for (int t0 = 0; t0 < steps; t0 += VT) {
         if (mine) put();
         wave_sync();
-#ifndef ACS_AB_NOLOAD      // A/B timing only (tools/build_variant.sh): tiles reuse the first inputs
         fetch(t0 + VT, mine ? t0 + VT + lane : steps);
-#endif
         for (int u = 0; u < 2; u++) {
             const int tw = t0 + u * WS;
             if (tw >= steps) break;
@@ -767,11 +707,9 @@ constexpr int TB_ROW = 65;
 // chunk and register ring for two waves per SIMD: measured slower, 0.41 vs 0.37 ms)
 constexpr int TB_CW = 64;
 constexpr int TB_LD = TB_CW / 4;            // 16-byte loads per lane per chunk
-#ifndef TB_RING
-#define TB_RING 3                          // decision chunks in the register ring (A/B hook: 4 and 5
-                                           // measured no faster, profiles/r02_acs_ab.txt -- the
-                                           // compiler waits vmcnt(0) at each staging anyway)
-#endif
+constexpr int TB_RING = 3;                  // decision chunks in the register ring (4 and 5 measured
+                                           // no faster, profiles/r02_acs_ab.txt -- the compiler waits
+                                           // vmcnt(0) at each staging anyway)
 constexpr int TB_WORDS = TB_CW * TB_ROW;    // one chunk of a wave's codewords
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TB_GROUP = 8;                 // chunks per output flush (240 bits per codeword)
@@ -846,13 +784,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
     // chunks of 16 KB per wave in flight while one is walked): the walk itself is short,
     // the loads are not
     u32x4 rr[TB_RING][TB_LD];
-#ifdef TB_AB_NOLOAD          // A/B timing only: chunks after the ring's first fill re-walk stale words
-    auto ld = [&](u32x4 (&r)[TB_LD], int ch) {
-        if (ch >= nch - TB_RING) tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane);
-    };
-#else
     auto ld = [&](u32x4 (&r)[TB_LD], int ch) { tb_load(r, blk0 + (int64_t)(ch > 0 ? ch : 0) * cstride, lane); };
-#endif
     // Decoded bits leave in groups of TB_GROUP chunks (240 bytes per codeword, 16-byte
     // stores): vector-memory stores pending beside the decision prefetches make the
     // compiler wait for every outstanding load (vmcnt(0)), so they come rarely.
