@@ -407,6 +407,60 @@ static int get_samples(orc_src *s, cf *v, int n, int32_t phase) {  /* ofdm-proce
     return 1;
 }
 
+/* ofdmProcessor::run's null search with scanMode (ofdm-processor.cpp:259-338): attempts
+ * counted at notSynced (:274), reset when a dip is found (:318); a search that gives up
+ * after T_F samples emits No_Signal_Found and restarts the count when scanMode and
+ * attempts > 5 (:310-315).  Runs over iq[0, n) until the samples run out (the
+ * reference's getSample blocks there: *attempts / *no_signal are its state at that
+ * point) or the end of a null is found (returns 1, *pos = the sample after it: where
+ * SyncOnPhase starts).  coarse + fine = 0. */
+int orc_null_scan(const float *iq, int64_t n, int scan, int32_t *attempts, int32_t *no_signal, int64_t *pos) {
+    tables_init();
+    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0};
+    float *envBuffer = (float *)malloc(sizeof(float) * 32768);
+    const int mask = 32768 - 1;
+    int idx, ret = 0;
+    float cur;
+    int32_t counter, att = 0, ns = 0;
+    cf smp;
+notSynced:
+    att++;
+    s.sLevel = 0;
+    for (int i = 0; i < 20 * ORC_TS; i++) if (!get_sample(&s, 0, &smp)) goto done;
+    idx = 0; cur = 0;
+    for (int i = 0; i < 50; i++) {
+        if (!get_sample(&s, 0, &smp)) goto done;
+        envBuffer[idx] = jan_abs(smp); cur += envBuffer[idx]; idx++;
+    }
+    counter = 0;
+    while (cur / 50 > 0.40 * s.sLevel) {
+        if (!get_sample(&s, 0, &smp)) goto done;
+        envBuffer[idx] = jan_abs(smp);
+        cur += envBuffer[idx] - envBuffer[(idx - 50) & mask];
+        idx = (idx + 1) & mask;
+        if (++counter > ORC_TF) {
+            if (scan && att > 5) { ns++; att = 0; }
+            goto notSynced;
+        }
+    }
+    att = 0;
+    counter = 0;
+    while (cur / 50 < 0.75 * s.sLevel) {
+        if (!get_sample(&s, 0, &smp)) goto done;
+        envBuffer[idx] = cabs_f(smp);
+        cur += envBuffer[idx] - envBuffer[(idx - 50) & mask];
+        idx = (idx + 1) & mask;
+        if (++counter > ORC_TNULL + 50) goto notSynced;
+    }
+    ret = 1;
+done:
+    free(envBuffer);
+    *attempts = att;
+    *no_signal = ns;
+    if (pos) *pos = s.pos;
+    return ret;
+}
+
 static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
                          orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf);
 int orc_ofdm_run(const float *iq, int64_t n, int16_t threshold, int method,

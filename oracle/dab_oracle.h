@@ -70,6 +70,9 @@ typedef struct {
     int32_t lp_window;      /* localPhase before the window's first sample */
 } orc_frame_info;
 
+/* ofdmProcessor::run's null search in scan mode: attempts / No_Signal_Found count when
+ * the samples run out (0) or where a null's end is found (1, pos) */
+int     orc_null_scan(const float *iq, int64_t n, int scan, int32_t *attempts, int32_t *no_signal, int64_t *pos);
 int     orc_ofdm_run(const float *iq /*cf32[n]*/, int64_t n, int16_t threshold, int method,
                      int max_frames, orc_frame_info *info, int16_t *softbits /*[max_frames][75][3072]*/);
 

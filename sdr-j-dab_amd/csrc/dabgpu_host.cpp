@@ -760,6 +760,7 @@ struct StreamSt {
     int32_t last_si = 504;
     int32_t resyncs = 0;
     int32_t attempts = 0;        // ofdmProcessor::run's `attempts` (ofdm-processor.cpp:274-314)
+    bool in_attempt = false;     // a null search cut by the end of the samples: `attempts` counts it
     int32_t no_signal = 0;       // No_Signal_Found emissions (scan mode)
     int32_t frames_run = 0;      // frames committed by the last dabgpu_pipe_run
     int32_t acquisitions = 0;    // null-symbol searches completed
@@ -1079,7 +1080,8 @@ static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         j.end = n_avail[s];
         j.local_phase = cur[s].lp;
         j.phase = cur[s].coarse + cur[s].fine;
-        j.attempts = cur[s].attempts;
+        // the kernel enters notSynced (attempts++) first; a cut attempt is repeated whole
+        j.attempts = cur[s].attempts - (cur[s].in_attempt ? 1 : 0);
         j.scan = p->scan ? 1 : 0;
         jobs.push_back(j);
     }
@@ -1097,6 +1099,7 @@ static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         S.lp = res[i].local_phase;
         S.window = res[i].window;
         S.attempts = res[i].attempts;
+        S.in_attempt = res[i].status != 0;
         S.no_signal += res[i].no_signal;
         if (res[i].status == 0) {
             S.synced = true;

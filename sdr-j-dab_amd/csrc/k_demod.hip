@@ -28,6 +28,7 @@ namespace dab {
 
 constexpr int DT = 256;                 // threads per demod workgroup
 constexpr int ZROW = 36;                // pass-2 output rows of 32 (+4 pad: conflict-free pass-3 reads)
+constexpr int EXN = 2048 + 64 * (ZROW - 32);   // FFT exchange buffer (float2)
 #ifndef DEMOD_WG_PER_SIMD
 #define DEMOD_WG_PER_SIMD 4     // resident workgroups per CU (= waves per SIMD): <= 128 VGPRs, <= 40 KB LDS
 #endif
@@ -343,13 +344,13 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                                                     OfdmTables T, int16_t *__restrict__ soft,
                                                     float *__restrict__ softf, float2 *__restrict__ fcpart,
                                                     DemodAux aux) {
-    __shared__ __attribute__((aligned(16))) float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ __attribute__((aligned(16))) float2 ex[EXN];
     // the soft-bit stage and the FreqCorr partials reuse the FFT exchange buffer (after
     // the FFT's last LDS pass, behind a barrier): 40 KB per workgroup with the NCO
     // tables, so 4 workgroups per CU
     uint32_t *st = (uint32_t *)ex;
-    float2 *fcw = ex;
     static_assert(STG * 4 <= sizeof(ex), "stage fits the exchange buffer");
+    float2 *fcw = ex;
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x;
@@ -449,6 +450,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             const int16_t v = snr_wg(a, t, red);
             if (t == 0) aux.snr[fi] = v;
         }
+        __syncthreads();                                // pass 3 read ex: the first symbol's pass 1 writes it
 #pragma unroll
         for (int k = 0; k < 8; k++) P[k] = a[k];
         // NCO of segment B: localPhase index of this thread's sample 0 of symbol l, stepped
@@ -577,7 +579,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
 template <bool GEN>
 __global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
                                                OfdmTables T, DemodAux aux) {
-    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ float2 ex[EXN];
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x, f = blockIdx.x;
@@ -616,7 +618,7 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
                                                   OfdmTables T, int method, int16_t *__restrict__ correction,
                                                   int16_t *__restrict__ snr) {
 #pragma clang fp contract(off)
-    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ float2 ex[EXN];
     __shared__ TwLds twl;
     __shared__ RedLds red;
     __shared__ float val[2048];                          // |X| (method 0) or per-candidate sums
@@ -725,7 +727,7 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
 // the previous spectrum in natural bin order.  One workgroup.
 __global__ __launch_bounds__(DT) void k_symbol_wg(const float2 *__restrict__ smp, int kind, OfdmTables T,
                                                   float2 *__restrict__ spec, int16_t *__restrict__ ibits) {
-    __shared__ float2 ex[2048 + 64 * (ZROW - 32)];
+    __shared__ float2 ex[EXN];
     __shared__ TwLds twl;
     const int t = threadIdx.x;
     const DemodTw tw = tw_setup(twl, T, t);

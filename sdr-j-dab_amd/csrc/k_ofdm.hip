@@ -253,11 +253,12 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
             r.attempts = attempts;
         } else {
             // out of samples inside an attempt: the reference would block in getSample
-            // until more arrive; hand back the attempt's start so that the next call,
-            // with more samples, repeats it exactly (it enters notSynced again)
+            // until more arrive, with `attempts` counting this attempt; hand back the
+            // attempt's start so that the next call, with more samples, repeats it exactly
+            // (the host passes attempts - 1 in: it enters notSynced again)
             r.window = a;
             r.local_phase = lpa;
-            r.attempts = att_start - 1;
+            r.attempts = att_start;
         }
         res[blockIdx.x] = r;
     }

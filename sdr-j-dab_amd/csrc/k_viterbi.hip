@@ -378,15 +378,13 @@ __device__ __forceinline__ uint32_t renorm(uint32_t x) {
 // spread + 1020 < 2^15), so one packed subtract yields both codewords' decisions;
 // they shift down their half of w (dec_in), 15 steps per half-word, and are
 // unpacked to one word per codeword (step k at bit k) at the end of the word.
-template <int NP, bool FULL>
-__device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
+// rp[r]: this lane's branch-metric row of relabelling phase r in the tile table (set once
+// per kernel); U: the word's half of the tile -- each step's read is one ds_read_b64 at
+// an immediate offset, no address arithmetic per word
+template <int NP, bool FULL, int U>
+__device__ __forceinline__ void acs_word_cw(const uint32_t *const (&rp)[6], uint32_t (&x)[NP], int nst,
                                             uint32_t (&cw)[2 * NP]) {
     static_assert(WS == 30, "two collectors of 8 and 7 step pairs per decision word");
-    // the 6 per-phase row addresses once per word: each step's read is then one
-    // ds_read_b64 at an immediate offset
-    const uint32_t *rp[6];
-#pragma unroll
-    for (int r = 0; r < 6; r++) rp[r] = bm + row[r];
     uint32_t w[NP], w0[NP], dp[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) w[p] = dp[p] = 0;
@@ -397,7 +395,7 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (
         if (FULL || j < nst) {
             sfor<0, NP>([&](auto pc) {
                 constexpr int p = decltype(pc)::value;
-                const uint2 t = *(const uint2 *)(rp[rho] + p * 8 * BRS + 2 * j);
+                const uint2 t = *(const uint2 *)(rp[rho] + U * 2 * WS + p * 8 * BRS + 2 * j);
                 uint32_t A, B;
                 cand<(32 >> rho)>(x[p], t.x, t.y, A, B);
                 d[p] = as_u32(as_pk(B) - as_pk(A));
@@ -431,15 +429,30 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *bm, const uint32_t (
 // ... and its words stored at chunk offset o (rb[k] < 0: codeword k not stored)
 // (through a buffer descriptor: the word's 32-bit offset is wave-uniform, so the store
 // carries one lane offset register instead of a 64-bit address per lane)
-template <int NP, bool FULL>
-__device__ __forceinline__ void acs_word(const uint32_t *bm, const uint32_t (&row)[6], uint32_t (&x)[NP], int nst,
+template <int NP, bool FULL, int U>
+__device__ __forceinline__ void acs_word(const uint32_t *const (&rp)[6], uint32_t (&x)[NP], int nst,
                                          __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP], int64_t o, int lane) {
     uint32_t cw[2 * NP];
-    acs_word_cw<NP, FULL>(bm, row, x, nst, cw);
+    acs_word_cw<NP, FULL, U>(rp, x, nst, cw);
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++)
         if (rb[k] >= 0)
             __builtin_amdgcn_raw_buffer_store_b32(cw[k], drs, 4 * lane, (int)(4 * (rb[k] + o)), 0);
+}
+// the two words of a tile [t0, t0 + VT)
+template <int NP>
+__device__ __forceinline__ void acs_tile(const uint32_t *const (&rp)[6], uint32_t (&x)[NP], int t0, int steps,
+                                         __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP], int lane) {
+    const int64_t cstride = 64 * 64;                    // words per chunk of a 64-row block
+    sfor<0, 2>([&](auto uc) {
+        constexpr int u = decltype(uc)::value;
+        const int tw = t0 + u * WS;
+        if (tw < steps) {
+            const int64_t o = (int64_t)(tw / WS) * cstride;
+            if (tw + WS <= steps) acs_word<NP, true, u>(rp, x, WS, drs, rb, o, lane);
+            else acs_word<NP, false, u>(rp, x, steps - tw, drs, rb, o, lane);
+        }
+    });
 }
 
 // NP pairs of codewords per wave: codewords 2*NP*w .. 2*NP*w + 2*NP - 1 (logical order).
@@ -527,19 +540,15 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         wave_sync();
         if (lane < VT) put_bm(bm, lane, sv);
     };
-    const int64_t cstride = 64 * 64;
+    const uint32_t *rp[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) rp[r] = bm + row[r];
     fetch(0);
     for (int t0 = 0; t0 < steps; t0 += VT) {
         put(t0);
         wave_sync();
         if (t0 + VT < steps) fetch(t0 + VT);
-        for (int u = 0; u < 2; u++) {
-            const int tw = t0 + u * WS;
-            if (tw >= steps) break;
-            const int64_t o = (int64_t)(tw / WS) * cstride;
-            if (tw + WS <= steps) acs_word<1, true>(bm + 2 * WS * u, row, x, WS, drs, rb, o, lane);
-            else acs_word<1, false>(bm + 2 * WS * u, row, x, steps - tw, drs, rb, o, lane);
-        }
+        acs_tile<1>(rp, x, t0, steps, drs, rb, lane);
         wave_sync();
     }
 }
@@ -677,19 +686,16 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 #pragma unroll
         for (int p = 0; p < NP; p++) put_bm(bm + p * 8 * BRS, lane, s[p]);
     };
+    const uint32_t *rp[6];
+#pragma unroll
+    for (int r = 0; r < 6; r++) rp[r] = bm + row[r];
     const bool mine = lane < VT;                         // lanes that build a step of the table
     fetch(0, mine ? lane : steps);
     for (int t0 = 0; t0 < steps; t0 += VT) {
         if (mine) put();
         wave_sync();
         fetch(t0 + VT, mine ? t0 + VT + lane : steps);
-        for (int u = 0; u < 2; u++) {
-            const int tw = t0 + u * WS;
-            if (tw >= steps) break;
-            const int64_t o = (int64_t)(tw / WS) * cstride;
-            if (tw + WS <= steps) acs_word<NP, true>(bm + 2 * WS * u, row, x, WS, drs, rb, o, lane);
-            else acs_word<NP, false>(bm + 2 * WS * u, row, x, steps - tw, drs, rb, o, lane);
-        }
+        acs_tile<NP>(rp, x, t0, steps, drs, rb, lane);
         wave_sync();
     }
     }

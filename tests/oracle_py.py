@@ -33,6 +33,7 @@ def oracle():
         _o.orc_process_block0.restype = C.c_int16
         _o.orc_rs_dec.restype = C.c_int16
         _o.orc_ofdm_run.argtypes = [C.c_void_p, C.c_int64, C.c_int16, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _o.orc_null_scan.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _o.orc_get_snr.restype = C.c_int16
         _o.orc_init()           # tables built once: the functions are then safe from threads
     return _o
@@ -80,6 +81,14 @@ def ofdm_run(iq, max_frames, threshold=3, method=1):
     soft = np.zeros((max_frames, 75, 3072), np.int16)
     n = oracle().orc_ofdm_run(P(iq), C.c_int64(len(iq) // 2), threshold, method, max_frames, info, P(soft))
     return n, list(info)[:n], soft[:n]
+
+
+def null_scan(iq, n, scan=True):
+    """ofdmProcessor::run's null search over iq[0, n) with scanMode (ofdm-processor.cpp:259-338):
+    (found, attempts, no_signal, pos) where the samples run out or a null's end is found"""
+    a, ns, pos = C.c_int32(), C.c_int32(), C.c_int64()
+    found = oracle().orc_null_scan(P(iq), C.c_int64(n), int(scan), C.byref(a), C.byref(ns), C.byref(pos))
+    return found, a.value, ns.value, pos.value
 
 
 def process_token(sym_ts, phase_ref):

@@ -270,3 +270,33 @@ def test_pipeline_solo_profiling_leaves_outputs_unchanged(ctx):
         d = ia["status"] == 3
         assert np.array_equal(sa[d], sb[d]), r
     assert outs[0][-1][3].any() and (outs[0][-1][4]["status"] == 3).any()
+
+
+def test_scan_mode_counts_attempts_like_reference(ctx):
+    """scanMode on a stream with no DAB signal (noise only), handed over in growing pieces
+    across several dabgpu_pipe_run calls: the null search gives up every T_F samples,
+    `attempts` counts the searches and No_Signal_Found fires after more than 5 of them
+    (ofdm-processor.cpp:274-315).  After every call the stream's attempts / no_signal
+    equal the reference's counters at the sample where its getSample would block
+    (oracle_py.null_scan), including an attempt cut in the middle by the end of the
+    available samples and resumed by the next call."""
+    import dabamd
+    rng = np.random.default_rng(7)
+    n = 3_400_000
+    iq = rng.normal(0.0, 0.3, 2 * n).astype(np.float32)
+    diq = ctx.put(iq)
+    pipe = dabamd.Pipeline(ctx, 1, 2, [])
+    try:
+        pipe.control(dabamd.CTL_SCAN_ON)
+        seen = []
+        for m in (200_000, 700_000, 1_250_000, 1_251_000, 1_600_000, 2_300_000, 3_000_000, 3_400_000):
+            pipe.run(diq, n, [m], partial=True)
+            st = pipe.state(0)
+            found, att, ns, pos = orc.null_scan(iq, m)
+            assert not found and not st.synced
+            assert (st.attempts, st.no_signal) == (att, ns), (m, st.attempts, st.no_signal, att, ns)
+            seen.append((att, ns))
+        assert seen[-1][1] >= 2 and any(a > 0 for a, _ in seen)   # the counters did move
+    finally:
+        pipe.close()
+        diq.free()
