@@ -115,6 +115,7 @@ void fib_processor::process_FIB(const uint8_t *p, uint16_t) {
         if (type == 7) return;
         if (type == 0) fig0(d);
         else if (type == 1) fig1(d);
+        else if (type == 2) fig2(d);
         processed += (int)bits(d, 3, 5) + 1;
         d = p + processed * 8;
     }
@@ -136,6 +137,9 @@ void fib_processor::fig0(const uint8_t *d) {
         break;
     case 14:
         fig0_14(d);
+        break;
+    case 16:
+        fig0_16(d);
         break;
     case 17:
         fig0_17(d);
@@ -193,17 +197,22 @@ int fib_processor::fig0_2(const uint8_t *d, int used, int pd) {
     o += 8;
     for (int i = 0; i < ncomp; i++) {
         const int8_t tmid = (int8_t)bits(d, o, 2);
-        component c;
+        // a new binding writes only these fields: the slot keeps whatever else its
+        // previous component left (sub-channel, DSCTy, ... until a FIG 0/3)
         if (tmid == 0) {                           // audio
-            c.ASCTy = (int16_t)bits(d, o + 2, 6);
-            c.subchannelId = (int16_t)bits(d, o + 8, 6);
-            c.PS_flag = (int16_t)bits(d, o + 14, 1);
-            bind(tmid, sid, (int16_t)i, c);
+            const int k = bind(tmid, sid, (int16_t)i);
+            if (k >= 0) {
+                components_[k].ASCTy = (int16_t)bits(d, o + 2, 6);
+                components_[k].subchannelId = (int16_t)bits(d, o + 8, 6);
+                components_[k].PS_flag = (int16_t)bits(d, o + 14, 1);
+            }
         } else if (tmid == 3) {                    // packet data
-            c.SCId = (uint16_t)bits(d, o + 2, 12);
-            c.PS_flag = (int16_t)bits(d, o + 14, 1);
-            c.CAflag = (uint8_t)bits(d, o + 15, 1);
-            bind(tmid, sid, (int16_t)i, c);
+            const int k = bind(tmid, sid, (int16_t)i);
+            if (k >= 0) {
+                components_[k].SCId = (uint16_t)bits(d, o + 2, 12);
+                components_[k].PS_flag = (int16_t)bits(d, o + 14, 1);
+                components_[k].CAflag = (uint8_t)bits(d, o + 15, 1);
+            }
         }
         o += 16;
     }
@@ -234,6 +243,13 @@ void fib_processor::fig0_14(const uint8_t *d) {
         for (subchannel &s : sub_)
             if (s.SubChId == id) s.FEC_scheme = fec;
     }
+}
+
+// fib-processor.cpp:707-724: the programme number is stored nowhere the lookups read,
+// but every SId gets a service entry
+void fib_processor::fig0_16(const uint8_t *d) {
+    const int len = (int)bits(d, 3, 5);
+    for (int o = 16; o < len * 8; o += 72) find_service((int32_t)bits(d, o, 16));
 }
 
 // fib-processor.cpp:726-752
@@ -282,10 +298,27 @@ void fib_processor::fig1(const uint8_t *d) {
         if (!s.hasName && charset <= 16) {
             read_label(ext == 1 ? 32 : 48);
             s.label += label_text(raw, 16, charset);
-            if (ext == 5) s.label += " (data)";     // addtoEnsemble only without MSC_DATA__ for 1/5
-            else if (svc_cb_) svc_cb_(s.label);
+            if (ext == 5) {                          // addtoEnsemble only without MSC_DATA__ for 1/5
+                static const uint8_t suffix[8] = {' ', '(', 'd', 'a', 't', 'a', ')', 0};
+                s.label += label_text(suffix, 8, charset);
+            } else if (svc_cb_) {
+                svc_cb_(s.label);
+            }
             s.hasName = true;
         }
+    }
+}
+
+// fib-processor.cpp:998-1037: FIG 2 extension 5, a data service label (32-bit SId)
+void fib_processor::fig2(const uint8_t *d) {
+    const int charset = (int)bits(d, 8, 4);
+    if (bits(d, 13, 3) != 5) return;
+    service &s = services_[find_service((int32_t)bits(d, 16, 32))];
+    if (!s.hasName && charset <= 16) {
+        uint8_t raw[16];
+        for (int i = 0; i < 16; i++) raw[i] = (uint8_t)bits(d, 48 + 8 * i, 8);
+        s.label += label_text(raw, 16, charset);
+        s.hasName = true;
     }
 }
 
@@ -312,8 +345,9 @@ int fib_processor::find_packet_component(int16_t scid) const {
 }
 
 // bind_audioService / bind_packetService (fib-processor.cpp:1077-1140): once per
-// (service, component number), in the first free slot
-void fib_processor::bind(int8_t tmid, int32_t sid, int16_t compnr, const component &c) {
+// (service, component number), in the first free slot; returns the slot (-1: bound
+// already, or the table is full, where the reference writes slot -1)
+int fib_processor::bind(int8_t tmid, int32_t sid, int16_t compnr) {
     const int s = find_service(sid);
     int first_free = -1;
     for (int i = 0; i < 64; i++) {
@@ -321,15 +355,15 @@ void fib_processor::bind(int8_t tmid, int32_t sid, int16_t compnr, const compone
             if (first_free < 0) first_free = i;
             continue;
         }
-        if (components_[i].service == s && components_[i].componentNr == compnr) return;
+        if (components_[i].service == s && components_[i].componentNr == compnr) return -1;
     }
-    if (first_free < 0) return;                    // table full (the reference writes slot -1)
+    if (first_free < 0) return -1;
     component &k = components_[first_free];
-    k = c;
     k.inUse = true;
     k.TMid = tmid;
     k.service = s;
     k.componentNr = compnr;
+    return first_free;
 }
 
 // fib-processor.cpp:1142-1163
@@ -339,7 +373,11 @@ void fib_processor::setupforNewFrame() {
 void fib_processor::clearEnsemble() {
     for (component &c : components_) c = component();
     for (subchannel &s : sub_) s = subchannel();
-    for (service &s : services_) s = service();
+    for (service &s : services_) {                 // language / programType / hasLanguage stay
+        s.inUse = false;
+        s.serviceId = -1;
+        s.label.clear();
+    }
     ensemble_.clear();
     firstTime_ = true;
 }

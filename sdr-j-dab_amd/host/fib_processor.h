@@ -16,13 +16,19 @@
 //   FIG 0/14 FEC scheme (the reference matches ficList[i].SubChId, which FIG 0/1
 //            never sets: only sub-channel id 0 takes effect, for every entry)  :688-705
 //   FIG 0/17 programme type and language                           :726-752
+//   FIG 0/16 programme number: only its service-table side effect (a new entry per
+//            unknown SId, which orders later lookups)              :707-724
 //   FIG 1/0  ensemble label, FIG 1/1 service label, FIG 1/5 data service label
 //            (" (data)" appended)                                  :850-997
+//   FIG 2/5  data service label, as FIG 1/5 without the suffix     :998-1037
+// clearEnsemble keeps a service entry's language and programme type, as the
+// reference's does (:1149-1163): an entry reused for a new service without FIG 0/17
+// reports the old values.
 // Labels are converted from the EBU Latin repertoire (charsets.cpp) or taken as
 // UTF-8 (charset 15) and returned as UTF-8 strings, 16 characters as transmitted
 // (trailing spaces included: the reference compares the full label).
-// The remaining FIG 0 extensions (0, 5, 6, 8, 9, 10, 13, 16, 18, 19, 21, 22) carry
-// nothing the service lookups read and are skipped; FIG 2 likewise.
+// The remaining FIG 0 extensions (0, 5, 6, 8, 9, 10, 13, 18, 19, 21, 22) carry
+// nothing the service lookups read and are skipped.
 #pragma once
 #include <cstdint>
 #include <functional>
@@ -110,10 +116,12 @@ private:
     int fig0_2(const uint8_t *d, int used, int pd);
     int fig0_3(const uint8_t *d, int used);
     void fig0_14(const uint8_t *d);
+    void fig0_16(const uint8_t *d);
     void fig0_17(const uint8_t *d);
+    void fig2(const uint8_t *d);
     int find_service(int32_t sid);
     int find_packet_component(int16_t scid) const;
-    void bind(int8_t TMid, int32_t sid, int16_t compnr, const component &c);
+    int bind(int8_t TMid, int32_t sid, int16_t compnr);
     int lookup(const std::string &label) const;       // first named service with this label
 
     service services_[64];

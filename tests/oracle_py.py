@@ -332,3 +332,298 @@ class Datagroups:
                 self.state, self.series = 1, list(take)
             else:
                 self.state, self.series = 0, []
+
+
+# ---- FIG parser: fib-processor.cpp restated (TEST INFRASTRUCTURE) ----------------
+# ETSI EN 300 401 table 8 (fib-processor.cpp:32-95): (CUs, protection level, kbit/s)
+UEP_TABLE = [
+    (16, 5, 32), (21, 4, 32), (24, 3, 32), (29, 2, 32), (35, 1, 32),
+    (24, 5, 48), (29, 4, 48), (35, 3, 48), (42, 2, 48), (52, 1, 48),
+    (29, 5, 56), (35, 4, 56), (42, 3, 56), (52, 2, 56),
+    (32, 5, 64), (42, 4, 64), (48, 3, 64), (58, 2, 64), (70, 1, 64),
+    (40, 5, 80), (52, 4, 80), (58, 3, 80), (70, 2, 80), (84, 1, 80),
+    (48, 5, 96), (58, 4, 96), (70, 3, 96), (84, 2, 96), (104, 1, 96),
+    (58, 5, 112), (70, 4, 112), (84, 3, 112), (104, 2, 112),
+    (64, 5, 128), (84, 4, 128), (96, 3, 128), (116, 2, 128), (140, 1, 128),
+    (80, 5, 160), (104, 4, 160), (116, 3, 160), (140, 2, 160), (168, 1, 160),
+    (96, 5, 192), (116, 4, 192), (140, 3, 192), (168, 2, 192), (208, 1, 192),
+    (116, 5, 224), (140, 4, 224), (168, 3, 224), (208, 2, 224), (232, 1, 224),
+    (128, 5, 256), (168, 4, 256), (192, 3, 256), (232, 2, 256), (280, 1, 256),
+    (160, 5, 320), (208, 4, 320), (280, 2, 320),
+    (192, 5, 384), (280, 3, 384), (416, 1, 384)]
+
+# EBU Latin based repertoire -> UCS-2 (ETSI TS 101 756 annex C; charsets.cpp:32-67):
+# identity except these code points
+_EBU_DIFF = {0x1f: 0x2d, 0x24: 0xa4, 0x5e: 0x2015, 0x60: 0x2551, 0x7e: 0xaf}
+_EBU_HI = [
+    0xe1, 0xe0, 0xe9, 0xe8, 0xed, 0xec, 0xf3, 0xf2, 0xfa, 0xf9, 0xd1, 0xc7, 0x15e, 0xdf, 0xa1, 0x132,
+    0xe2, 0xe4, 0xea, 0xeb, 0xee, 0xef, 0xf4, 0xf6, 0xfb, 0xfc, 0xf1, 0xe7, 0x15f, 0x11f, 0x131, 0x133,
+    0xaa, 0x3b1, 0xa9, 0x2030, 0x11e, 0x11b, 0x148, 0x151, 0x3c0, 0x20ac, 0xa3, 0x24, 0x2190, 0x2191, 0x2192, 0x2193,
+    0xba, 0xb9, 0xb2, 0xb3, 0xb1, 0x130, 0x144, 0x171, 0xb5, 0xbf, 0xf7, 0xb0, 0xbc, 0xbd, 0xbe, 0xa7,
+    0xc1, 0xc0, 0xc9, 0xc8, 0xcd, 0xcc, 0xd3, 0xd2, 0xda, 0xd9, 0x158, 0x10c, 0x160, 0x17d, 0xd0, 0x13f,
+    0xc2, 0xc4, 0xca, 0xcb, 0xce, 0xcf, 0xd4, 0xd6, 0xdb, 0xdc, 0x159, 0x10d, 0x161, 0x17e, 0x111, 0x140,
+    0xc3, 0xc5, 0xc6, 0x152, 0x177, 0xdd, 0xd5, 0xd8, 0xde, 0x14a, 0x154, 0x106, 0x15a, 0x179, 0x166, 0xf0,
+    0xe3, 0xe5, 0xe6, 0x153, 0x175, 0xfd, 0xf5, 0xf8, 0xfe, 0x14b, 0x155, 0x107, 0x15b, 0x17a, 0x167, 0xff]
+
+
+def charset_text(raw, charset):
+    """toQStringUsingCharset (charsets.cpp:69-95) of a NUL-terminated byte string:
+    UTF-8 (0x0F) decoded, EBU Latin (0x00 and every other value) mapped per byte
+    up to the first NUL.  (UCS-2, 0x06, reads past the reference's buffer when the
+    label has no zero pair: not restated.)"""
+    raw = bytes(raw)
+    if 0 in raw:
+        raw = raw[:raw.index(0)]
+    if charset == 0x0F:
+        return raw.decode("utf-8", "replace")
+    return "".join(chr(_EBU_HI[b - 0x80] if b >= 0x80 else _EBU_DIFF.get(b, b)) for b in raw)
+
+
+class FibProcessor:
+    """fib_processor (fib-processor.cpp) restated over the FIGs that reach the service
+    lookups: FIG 0/1, 0/2, 0/3, 0/14, 0/16, 0/17, 1/0, 1/1, 1/5, 2/5; the lookups
+    kindofService / dataforAudioService / dataforDataService; clearEnsemble /
+    setupforNewFrame.  Signals are recorded in `events` (("E", EId, name) for
+    nameofEnsemble, ("S", label) for addtoEnsemble)."""
+
+    UNKNOWN, AUDIO, PACKET = 0o100, 0o101, 0o102
+
+    def __init__(self):
+        self.services = [dict(inUse=False, serviceId=-1, hasName=False, label="", language=0,
+                              programType=0, hasLanguage=False) for _ in range(64)]
+        self.events = []
+        self.clearEnsemble()                                       # :98-114
+
+    @staticmethod
+    def _bits(d, off, n):                                          # getBits / getLBits (dab-constants.h:182-308)
+        v = 0
+        for i in range(n):
+            v = (v << 1) | (int(d[off + i]) & 1)
+        return v
+
+    def process_FIB(self, d):                                      # :123-158
+        done = 0
+        p = 0
+        while done < 30:
+            t = self._bits(d[p:], 0, 3)
+            if t == 7:
+                return
+            if t == 0:
+                self._fig0(d[p:])
+            elif t == 1:
+                self._fig1(d[p:])
+            elif t == 2:
+                self._fig2(d[p:])
+            done += self._bits(d[p:], 3, 5) + 1
+            p = done * 8
+
+    def _fig0(self, d):                                            # :162-239
+        ext = self._bits(d, 8 + 3, 5)
+        L = self._bits(d, 3, 5)
+        pd = self._bits(d, 8 + 2, 1)
+        if ext == 1:                                               # :278-286
+            used = 2
+            while used < L - 1:
+                used = self._fig0_1(d, used)
+        elif ext == 2:                                             # :356-367
+            used = 2
+            while used < L:
+                used = self._fig0_2(d, used, pd)
+        elif ext == 3:                                             # :424-431
+            used = 2
+            while used < L:
+                used = self._fig0_3(d, used)
+        elif ext == 14:                                            # :688-705
+            used = 2
+            while used < L:
+                sid = self._bits(d, used * 8, 6)
+                fec = self._bits(d, used * 8 + 6, 2)
+                used += 1
+                for f in self.ficList:
+                    if f["SubChId"] == sid:
+                        f["FEC_scheme"] = fec
+        elif ext == 16:                                            # :707-724
+            off = 16
+            while off < L * 8:
+                s = self._find_service(self._bits(d, off, 16))
+                if not s.get("hasPNum"):
+                    s["hasPNum"] = True
+                off += 72
+        elif ext == 17:                                            # :726-752
+            off = 16
+            while off < L * 8:
+                sid = self._bits(d, off, 16)
+                lflag = self._bits(d, off + 18, 1)
+                ccflag = self._bits(d, off + 19, 1)
+                s = self._find_service(sid)
+                if lflag:
+                    s["language"] = self._bits(d, off + 24, 8)
+                    s["hasLanguage"] = True
+                    off += 8
+                s["programType"] = self._bits(d, off + 27, 5)
+                off += 40 if ccflag else 32
+
+    def _fig0_1(self, d, used):                                    # :288-347
+        o = used * 8
+        sid = self._bits(d, o, 6)
+        f = self.ficList[sid]
+        f["StartAddr"] = self._bits(d, o + 6, 10)
+        if self._bits(d, o + 16, 1) == 0:
+            cus, lvl, rate = UEP_TABLE[self._bits(d, o + 18, 6)]
+            f.update(Length=cus, uepFlag=0, protLevel=lvl, BitRate=rate)
+            o += 24
+        else:
+            f["uepFlag"] = 1
+            option = self._bits(d, o + 17, 3)
+            lvl = self._bits(d, o + 20, 2) + 1
+            size = self._bits(d, o + 22, 10)
+            if option == 0:
+                f["protLevel"] = lvl + 0o100
+                f["Length"] = size
+                f["BitRate"] = size // {1: 12, 2: 8, 3: 6, 4: 4}[lvl] * 8
+            elif option == 1:
+                f["protLevel"] = lvl + 0o200
+                f["Length"] = size
+                f["BitRate"] = size // {1: 27, 2: 21, 3: 18, 4: 15}[lvl] * 32
+            o += 32
+        return o // 8
+
+    def _fig0_2(self, d, used, pd):                                # :377-418
+        o = used * 8
+        if pd == 1:
+            sid = self._bits(d, o, 32)
+            o += 32
+        else:
+            sid = self._bits(d, o, 16)
+            o += 16
+        sid = sid - (1 << 32) if sid >= 1 << 31 else sid           # int32_t SId
+        n = self._bits(d, o + 4, 4)
+        o += 8
+        for i in range(n):
+            tmid = self._bits(d, o, 2)
+            if tmid == 0:
+                self._bind(0, sid, i, dict(ASCTy=self._bits(d, o + 2, 6), subchannelId=self._bits(d, o + 8, 6),
+                                           PS_flag=self._bits(d, o + 14, 1)))
+            elif tmid == 3:
+                self._bind(3, sid, i, dict(SCId=self._bits(d, o + 2, 12), PS_flag=self._bits(d, o + 14, 1),
+                                           CAflag=self._bits(d, o + 15, 1)))
+            o += 16
+        return o // 8
+
+    def _fig0_3(self, d, used):                                    # :433-453
+        o = used * 8
+        scid = self._bits(d, o, 12)
+        for c in self.components:                                  # find_packetComponent (:1060-1072)
+            if c["inUse"] and c["TMid"] == 3 and c["SCId"] == scid:
+                c.update(subchannelId=self._bits(d, o + 24, 6), DSCTy=self._bits(d, o + 18, 6),
+                         DGflag=self._bits(d, o + 16, 1), packetAddress=self._bits(d, o + 30, 10))
+                break
+        return used + 7
+
+    def _label(self, d, off, charset):
+        return charset_text([self._bits(d, off + 8 * i, 8) for i in range(16)], charset)
+
+    def _fig1(self, d):                                            # :850-994
+        charset = self._bits(d, 8, 4)
+        oe = self._bits(d, 12, 1)
+        ext = self._bits(d, 13, 3)
+        if ext == 0:
+            eid = self._bits(d, 16, 16)
+            if charset <= 16 and not oe:
+                name = self._label(d, 32, charset)
+                if self.firstTime:
+                    self.events.append(("E", eid, name))
+                self.firstTime = False
+        elif ext in (1, 5):
+            sid = self._bits(d, 16, 16) if ext == 1 else self._bits(d, 16, 32)
+            sid = sid - (1 << 32) if sid >= 1 << 31 else sid
+            s = self._find_service(sid)
+            if not s["hasName"] and charset <= 16:
+                s["label"] += self._label(d, 32 if ext == 1 else 48, charset)
+                if ext == 5:
+                    s["label"] += charset_text(b" (data)\0", charset)
+                else:
+                    self.events.append(("S", s["label"]))
+                s["hasName"] = True
+
+    def _fig2(self, d):                                            # :998-1037
+        charset = self._bits(d, 8, 4)
+        if self._bits(d, 13, 3) == 5:
+            sid = self._bits(d, 16, 32)
+            sid = sid - (1 << 32) if sid >= 1 << 31 else sid
+            s = self._find_service(sid)
+            if not s["hasName"] and charset <= 16:
+                s["label"] += self._label(d, 48, charset)
+                s["hasName"] = True
+
+    def _find_service(self, sid):                                  # :1041-1058
+        for s in self.services:
+            if s["inUse"] and s["serviceId"] == sid:
+                return s
+        for s in self.services:
+            if not s["inUse"]:
+                s.update(inUse=True, hasName=False, serviceId=sid)
+                return s
+        return self.services[0]
+
+    def _bind(self, tmid, sid, compnr, fields):                    # :1077-1139
+        s = self.services.index(self._find_service(sid))
+        first = -1
+        for i, c in enumerate(self.components):
+            if not c["inUse"]:
+                if first < 0:
+                    first = i
+                continue
+            if c["service"] == s and c["componentNr"] == compnr:
+                return
+        c = self.components[first]
+        c.update(fields)
+        c.update(inUse=True, TMid=tmid, service=s, componentNr=compnr)
+
+    def setupforNewFrame(self):                                    # :1142-1147
+        for c in self.components:
+            c["inUse"] = False
+
+    def clearEnsemble(self):                                       # :1149-1163
+        self.components = [dict(inUse=False, TMid=0, componentNr=0, service=-1, subchannelId=0, PS_flag=0,
+                                ASCTy=0, SCId=0, CAflag=0, DSCTy=0, DGflag=0, packetAddress=0) for _ in range(64)]
+        self.ficList = [dict(SubChId=0, StartAddr=0, Length=0, uepFlag=0, protLevel=0, BitRate=0, FEC_scheme=0)
+                        for _ in range(64)]
+        for s in self.services:                                    # language / programType survive
+            s.update(inUse=False, serviceId=-1, label="")
+        self.firstTime = True
+
+    def labels(self):
+        return [s["label"] for s in self.services if s["inUse"] and s["hasName"]]
+
+    def _lookup(self, label, want):
+        for s in self.services:                                    # :1197-1315
+            if not s["inUse"] or not s["hasName"] or s["label"] != label:
+                continue
+            for c in self.components:
+                if not c["inUse"] or self.services[c["service"]]["serviceId"] != s["serviceId"]:
+                    continue
+                if want == "kind":
+                    if c["TMid"] == 3:
+                        return self.PACKET
+                    if c["TMid"] == 0:
+                        return self.AUDIO
+                    continue
+                if c["TMid"] != (0 if want == "audio" else 3):
+                    return None                                    # "fatal error, expected ..."
+                f = self.ficList[c["subchannelId"]]
+                if want == "audio":
+                    return [c["subchannelId"], f["StartAddr"], f["uepFlag"], f["protLevel"], f["Length"],
+                            f["BitRate"], c["ASCTy"], s["language"], s["programType"]]
+                return [c["subchannelId"], f["StartAddr"], f["uepFlag"], f["protLevel"], c["DSCTy"], f["Length"],
+                        f["BitRate"], f["FEC_scheme"], c["DGflag"], c["packetAddress"]]
+        return self.UNKNOWN if want == "kind" else None
+
+    def kindofService(self, label):
+        return self._lookup(label, "kind")
+
+    def dataforAudioService(self, label):
+        return self._lookup(label, "audio")
+
+    def dataforDataService(self, label):
+        return self._lookup(label, "data")
