@@ -16,7 +16,7 @@ class SynthSubch(C.Structure):
                 ("protLevel", C.c_int16), ("uep", C.c_int16), ("dabplus", C.c_int16), ("content", C.c_int16)]
 
 
-MP2, PACKET = 2, 3   # SynthSubch.content (dabsynth.h DABSYNTH_MP2 / DABSYNTH_PACKET)
+MP2, PACKET, AU_MIX = 2, 3, 4   # SynthSubch.content (dabsynth.h DABSYNTH_MP2 / _PACKET / _AU_MIX)
 
 
 class SynthCfg(C.Structure):
@@ -51,7 +51,8 @@ def _p(a):
 class Ensemble:
     """Synthetic ensemble generator.  subch: tuples (startAddr, length, bitRate,
     protLevel, uep, dabplus[, content]) -- uep=1 for UEP (uepFlag 0 in the reference);
-    content MP2 / PACKET for MPEG layer II frames / packet-mode data groups."""
+    content MP2 / PACKET for MPEG layer II frames / packet-mode data groups; AU_MIX
+    on a DAB+ subchannel cycles its superframes through the 4 (dacRate, SBR) layouts."""
 
     def __init__(self, n_frames: int, subch: Sequence[tuple] = (), pre_offset: int = 50000,
                  snr_db: float = 300.0, cfo_hz: float = 0.0, amplitude: float = 1.0, figs: bool = False):

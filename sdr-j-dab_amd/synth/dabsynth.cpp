@@ -241,22 +241,36 @@ uint16_t fire_parity(const uint8_t *x) {
     return st;
 }
 
-void make_superframe(Rng &rng, int rsdims, uint8_t *sf /*[120*rsdims]*/) {
+static const int kAuCount[4] = {4, 2, 6, 3}, kAuFirst[4] = {8, 5, 11, 6};
+// an even split of a superframe into layout's AUs passes the reference's checks
+// (mp4processor.cpp:197-205: length < 960; start addresses fit 12 bits)
+static bool superframe_layout_ok(int rsdims, int layout) {
+    const int n = 110 * rsdims, nau = kAuCount[layout], first = kAuFirst[layout], span = n - first;
+    return span / nau + 1 < 960 - 2 && first + span * (nau - 1) / nau < 4096;
+}
+
+// one DAB+ superframe of rsdims RS columns; layout = 2 * dacRate + sbr: 4, 2, 6 or 3
+// access units whose start addresses the header carries (12 bits each after byte 3,
+// the first one implicit: mp4processor.cpp:163-195)
+void make_superframe(Rng &rng, int rsdims, uint8_t *sf /*[120*rsdims]*/, int layout = 0) {
     int n = 110 * rsdims;
     std::vector<uint8_t> d(n);
     for (auto &b : d) b = (uint8_t)rng.next();
-    // header: dacRate 0, sbr 0 -> 4 AUs starting at byte 8
-    d[2] = (uint8_t)(d[2] & 0x80);          // dacRate=0 sbr=0 ch=0 ps=0 surround=0
-    int au[5];
-    au[0] = 8; au[4] = n;
-    int span = n - 8;
-    au[1] = 8 + span / 4; au[2] = 8 + span / 2; au[3] = 8 + 3 * span / 4;
-    d[3] = (uint8_t)(au[1] >> 4);
-    d[4] = (uint8_t)(((au[1] & 0xf) << 4) | ((au[2] >> 8) & 0xf));
-    d[5] = (uint8_t)(au[2] & 0xff);
-    d[6] = (uint8_t)(au[3] >> 4);
-    d[7] = (uint8_t)(((au[3] & 0xf) << 4) | (d[7] & 0xf));
-    for (int i = 0; i < 4; i++) {
+    const int nau = kAuCount[layout & 3], first = kAuFirst[layout & 3];
+    d[2] = (uint8_t)((d[2] & 0x80) | ((layout & 3) << 5));   // dacRate, sbr; ch=0 ps=0 surround=0
+    int au[7];
+    au[0] = first;
+    au[nau] = n;
+    const int span = n - first;
+    for (int i = 1; i < nau; i++) au[i] = first + span * i / nau;
+    for (int i = 1; i < nau; i++) {                   // 12-bit start addresses, MSB first from byte 3
+        const int bit = 24 + 12 * (i - 1);
+        for (int b = 0; b < 12; b++) {
+            const int pos = bit + b, v = (au[i] >> (11 - b)) & 1;
+            d[pos >> 3] = (uint8_t)((d[pos >> 3] & ~(0x80 >> (pos & 7))) | (v << (7 - (pos & 7))));
+        }
+    }
+    for (int i = 0; i < nau; i++) {
         int len = au[i + 1] - au[i] - 2;
         uint16_t c = (uint16_t)~crc_ccitt(&d[au[i]], len);
         d[au[i] + len] = (uint8_t)(c >> 8);
@@ -503,12 +517,25 @@ static int gen_core(const dabsynth_cfg *cfg, uint64_t seed, int P, float *iq, ui
         // dabplus = 1 + k: the superframe grid is shifted by k CIFs (k = 1..4 makes the
         // receiver's first five CIFs straddle two superframes)
         int sf_pos = sc.dabplus > 1 ? ((sc.dabplus - 1) % 5) * (nb / 8) : 0;
+        int sf_count = 0;                                 // superframes made (AU layout cycle)
         for (int e = e0; e < NC; e++) {
             if (sc.dabplus) {
                 // 5 CIFs carry one superframe; superframes start at e = e0 + 5m
                 int per = nb / 8;
                 for (int byte = 0; byte < per; byte++) {
-                    if (sf_pos == 0) make_superframe(rng, rsdims, sf.data());
+                    if (sf_pos == 0) {
+                        int layout = 0;
+                        if (sc.content == DABSYNTH_AU_MIX) {
+                            // the next layout (cycling) whose AUs the reference accepts at
+                            // this size: each < 960 bytes, 12-bit start addresses
+                            for (int k = 0; k < 4; k++) {
+                                const int l = (sf_count + k) & 3;
+                                if (superframe_layout_ok(rsdims, l)) { layout = l; break; }
+                            }
+                            sf_count++;
+                        }
+                        make_superframe(rng, rsdims, sf.data(), layout);
+                    }
                     uint8_t v = sf[sf_pos];
                     for (int b = 0; b < 8; b++) info[8 * byte + b] = (uint8_t)((v >> (7 - b)) & 1);
                     sf_pos = (sf_pos + 1) % (120 * rsdims);

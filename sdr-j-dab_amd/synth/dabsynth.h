@@ -32,10 +32,14 @@ typedef struct {
                             CIF (48 kHz, sync + header, payload bytes < 0x80 so only headers carry
                             12 ones in a row); DABSYNTH_PACKET: packet mode, 24..96-byte packets with
                             CRCs carrying MSC data groups (address 0x100 + subchannel index, some
-                            padding packets), announced as DSCTy 60 by FIG 0/2 (TMid 3) + FIG 0/3 */
+                            padding packets), announced as DSCTy 60 by FIG 0/2 (TMid 3) + FIG 0/3;
+                            with dabplus: 0 every superframe dacRate 0 / SBR 0 (4 AUs),
+                            DABSYNTH_AU_MIX the superframes cycle through the four (dacRate, SBR)
+                            layouts of mp4processor.cpp:163-195 (4, 2, 6, 3 AUs) */
 } dabsynth_subch;
 #define DABSYNTH_MP2 2
 #define DABSYNTH_PACKET 3
+#define DABSYNTH_AU_MIX 4
 
 typedef struct {
     int32_t n_frames;    /* frames after the pre-roll */

@@ -403,12 +403,30 @@ def test_pipeline_dabplus_matches_oracle(ctx, snr):
     """mp4Processor per DAB+ subchannel (mp4processor.cpp:107-292) after the GPU MSC
     decode: per CIF status, RS corrections, AU table and CRCs, superframe bytes --
     against the oracle's state machine fed with the same decoded MSC bits."""
-    import dabamd
-    from dabamd.synth import Ensemble
     # (startAddr, CUs, kbps, level, uep, dabplus = 1 + grid shift)
     subch = [(0, 32, 64, 0o104, 0, 1), (32, 72, 96, 0o103, 0, 4), (104, 96, 128, 3, 1, 0),
              (200, 24, 48, 0o104, 0, 2)]
-    F, runs, S = 3, 3, 2
+    _dabplus_vs_oracle(ctx, snr, subch)
+
+
+@pytest.mark.parametrize("snr", [300.0, 10.5])
+def test_pipeline_dabplus_au_layouts_match_oracle(ctx, snr):
+    """As above with the superframes cycling through the four (dacRate, SBR) AU layouts
+    (mp4processor.cpp:163-195: 4, 2, 6 and 3 AUs; the transmitter's AU_MIX) at 32, 64,
+    128 and 192 kbit/s (RS widths 4 to 24): AU counts, start addresses and CRCs of every
+    layout against the oracle."""
+    from dabamd.synth import AU_MIX
+    subch = [(0, 32, 32, 0o102, 0, 1, AU_MIX), (32, 48, 64, 0o103, 0, 3, AU_MIX),
+             (80, 96, 128, 0o103, 0, 2, AU_MIX), (176, 144, 192, 0o103, 0, 5, AU_MIX)]
+    layouts = _dabplus_vs_oracle(ctx, snr, subch, runs=4)
+    assert layouts >= ({2, 3, 4, 6} if snr > 100 else {4}), layouts
+
+
+def _dabplus_vs_oracle(ctx, snr, subch, runs=3):
+    import dabamd
+    from dabamd.synth import Ensemble
+    F, S = 3, 2
+    layouts = set()
     e = Ensemble(F * runs, subch=subch, snr_db=snr)
     gens = [e.generate(s) for s in (21, 22)]
     iq = np.stack([g["iq"] for g in gens])
@@ -440,6 +458,7 @@ def test_pipeline_dabplus_matches_oracle(ctx, snr):
                     if o["status"] == 3:
                         n3 += 1
                         na = o["num_aus"]
+                        layouts.add(na)
                         assert np.array_equal(rec["au_start"][:na + 1], o["au_start"][:na + 1])
                         assert rec["au_crc_ok"] == sum(int(o["au_crc"][a]) << a for a in range(na))
                         nb = 110 * (br // 8)
@@ -447,3 +466,4 @@ def test_pipeline_dabplus_matches_oracle(ctx, snr):
     assert n3 >= S * len(dpi) * 2 if snr > 100 else n3 > 0
     pipe.close()
     diq.free()
+    return layouts

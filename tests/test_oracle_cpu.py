@@ -193,6 +193,34 @@ def test_oracle_dabplus_superframe():
     assert good >= 2
 
 
+def test_oracle_superframe_au_layouts():
+    """The transmitter's AU_MIX superframes (dacRate / SBR cycling through the four
+    layouts of mp4processor.cpp:163-195: 4, 2, 6, 3 access units, where their AUs fit the
+    reference's limits) decode in the oracle's superframe restatement with every AU CRC
+    good, at RS widths 4 (32 kbit/s) to 24 (192 kbit/s: no 2-AU layout, its AUs would
+    exceed 960 bytes)."""
+    from dabamd.synth import AU_MIX, Ensemble
+    for br, cus, pl in ((32, 32, 0o102), (64, 48, 0o103), (128, 96, 0o103), (192, 144, 0o103)):
+        rs = br // 8
+        e = Ensemble(9, subch=[(0, cus, br, pl, 0, 1, AU_MIX)], snr_db=300.0)
+        g = e.generate(11)
+        bits = g["msc"][:, 0, :24 * br]
+        seen = []
+        for n0 in range(16, 4 * 9 - 4):
+            by = np.packbits(bits[n0:n0 + 5].reshape(-1))
+            if not orc.oracle().orc_firecode_check(P(by[:11])):
+                continue
+            out = np.zeros(110 * rs, np.uint8)
+            nc = C.c_int16()
+            na = C.c_int()
+            au = np.zeros(8, np.int16)
+            crc = np.zeros(8, np.uint8)
+            ok = orc.oracle().orc_superframe(P(by), 0, br, P(out), C.byref(nc), C.byref(na), P(au), P(crc))
+            assert ok == 1 and nc.value == 0 and crc[:na.value].all(), (br, n0, na.value)
+            seen.append(na.value)
+        assert set(seen) == ({3, 4, 6} if br == 192 else {2, 3, 4, 6}), (br, seen)
+
+
 def test_oracle_mp4_state_machine():
     """mp4Processor::addtoFrame (mp4processor.cpp:107-145): with the superframe grid
     shifted by 2 CIFs the fire code fails until the ring is aligned, then every
