@@ -55,13 +55,16 @@ MIXED = [(0, 96, 128, 3, 1), (96, 48, 64, 0o103, 0), (144, 24, 32, 0o104, 0), (1
 
 
 @pytest.mark.parametrize("snr,cfo,runs", [(11.0, 0.0, 3), (8.0, 0.0, 3), (12.0, 300.0, 8), (12.0, 800.0, 8),
-                                          (11.5, -1700.0, 8), (25.0, 2300.0, 3)])
+                                          (11.5, -1700.0, 8), (25.0, 2300.0, 3), (20.0, -9700.0, 4),
+                                          (20.0, 6400.0, 4)])
 def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs):
     """two ensembles, 5 subchannels (UEP-3/-2, EEP-3A/-4A, one above CU 511), runs of 4
     frames: every committed frame's placement/correctors, soft bits, FIC bits + CRCs and
     MSC bits against the oracle run on the same IQ.  8 dB is at the FIC's decoding
     threshold for this transmitter (CRC failures in both); with a CFO the fine AFC
-    converges by 10% per frame (ofdm-processor.cpp:445-446), hence 32 frames."""
+    converges by 10% per frame (ofdm-processor.cpp:445-446), hence 32 frames.  -9.7 and
+    +6.4 kHz are several carriers off: the coarse corrector (processBlock_0's offset,
+    ofdm-processor.cpp:395-406) has to move first."""
     F = 4
     iqs = _gen(MIXED, F * runs + 1, [31, 32], snr, cfo)
     refs = orc.decode_streams(iqs, F * runs, MIXED)
@@ -69,8 +72,8 @@ def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs):
     stats = [pc.compare(gpu[s], refs[s], MIXED) for s in range(2)]
     print(f"snr {snr} cfo {cfo}:", stats)
     _check(stats, (snr, cfo))
-    if cfo == 2300.0:
-        return                        # the reference's AFC wanders here; parity is what counts
+    if abs(cfo) > 2000.0:
+        return                        # the reference's AFC may wander here; parity is what counts
     for s in range(2):
         # the same frames as the reference (a stream that loses sync under a large
         # offset re-acquires inside the run and delivers fewer frames -- in both)
