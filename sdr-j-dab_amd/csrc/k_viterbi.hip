@@ -260,6 +260,11 @@ __device__ __forceinline__ int parity(int v) { return __popc(v) & 1; }
 // pattern); step j of row q holds the pair {bm[q], bm[q^7]} as two packed words
 // (codeword A in the low, B in the high 16 bits).  The row stride puts the 8 rows one
 // ds_read_b64 touches in 8 distinct bank pairs.
+// branch-metric pairs are read ACS_PF steps ahead of their use (round 3: 3 steps ahead
+// took k_acs2 1.31 -> 1.29 ms in the pipeline, profiles/r03_acs_pf_ab.txt; 2 and 4 no better)
+#ifndef ACS_PF
+#define ACS_PF 3
+#endif
 constexpr int WS = DEC_WORD_STEPS;         // 30 decisions per word: a multiple of 6, so
                                            // every word starts at relabelling phase 0
 constexpr int VT = 2 * WS;                 // steps per branch-metric tile (lanes 0..59 build one each)
@@ -319,7 +324,8 @@ __device__ __forceinline__ void cand(uint32_t x, uint32_t ta, uint32_t tb, uint3
         asm(DPP_ADD_NOP("quad_perm:[0,1,0,1] row_mask:0xf bank_mask:0xf") : "=&v"(A) : "v"(x), "v"(ta));
         asm(DPP_ADD("quad_perm:[2,3,2,3] row_mask:0xf bank_mask:0xf") : "=&v"(B) : "v"(x), "v"(tb));
     } else if constexpr (M == 16) {
-        // swizzle bit mode: lane' = (lane & and) | or within 32 lanes
+        // swizzle bit mode: lane' = (lane & and) | or within 32 lanes (a permlane16 swap
+        // instead measured no faster, round 3)
         A = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x0F) + ta;              // lane & ~16
         B = (uint32_t)__builtin_amdgcn_ds_swizzle((int)x, 0x1F | (0x10 << 5)) + tb; // lane | 16
     } else if constexpr (M == 4) {
@@ -388,14 +394,28 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *const (&rp)[6], uint
     uint32_t w[NP], w0[NP], dp[NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) w[p] = dp[p] = 0;
+    // branch-metric pairs read ACS_PF steps ahead of their use (the LDS latency off the
+    // metric chain)
+    constexpr int PF = ACS_PF;
+    uint2 tq[NP][PF + 1];
+    auto ldt = [&](int jj, int p) { return *(const uint2 *)(rp[jj % 6] + U * 2 * WS + p * 8 * BRS + 2 * jj); };
+    sfor<0, PF>([&](auto jc) {
+        constexpr int jj = decltype(jc)::value;
+#pragma unroll
+        for (int p = 0; p < NP; p++) tq[p][jj % (PF + 1)] = ldt(jj, p);
+    });
     sfor<0, WS>([&](auto jc) {
         constexpr int j = decltype(jc)::value;
         constexpr int rho = j % 6;
         uint32_t d[NP];
+        if constexpr (PF > 0 && j + PF < WS) {
+#pragma unroll
+            for (int p = 0; p < NP; p++) tq[p][(j + PF) % (PF + 1)] = ldt(j + PF, p);
+        }
         if (FULL || j < nst) {
             sfor<0, NP>([&](auto pc) {
                 constexpr int p = decltype(pc)::value;
-                const uint2 t = *(const uint2 *)(rp[rho] + U * 2 * WS + p * 8 * BRS + 2 * j);
+                const uint2 t = PF > 0 ? tq[p][j % (PF + 1)] : ldt(j, p);
                 uint32_t A, B;
                 cand<(32 >> rho)>(x[p], t.x, t.y, A, B);
                 d[p] = as_u32(as_pk(B) - as_pk(A));
