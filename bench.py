@@ -507,7 +507,14 @@ def main():
             return [stride] * E
         return [min(stride, got[0] * cs)] * E
 
+    # the initial null search of every stream (k_acquire, one wave per stream): the cost a
+    # sync loss pays before the pipeline resumes (ofdm-processor.cpp:298-357), reported beside
+    # the steady state, never inside the timed region
+    pipe.sync()
+    t_acq = time.perf_counter()
     pipe.acquire(diq, stride, [0] * E, avail())
+    pipe.sync()
+    acquire_ms = (time.perf_counter() - t_acq) * 1e3
 
     def step(k, download=False):
         # chunk k + 2 travels while step k decodes (the frames of step k need chunks <= k + 1)
@@ -634,6 +641,7 @@ def main():
         "checked_step": checks[0] if world == 1 else checks,
         "dabplus_last_step": sf_ok,
         "gen_seconds": gen_s,
+        "acquire_ms": {"streams": E, "ms": acquire_ms, "note": "initial null search of every stream (host-timed, first launch)"},
     }
     if probe is not None:
         out["stream_split"] = probe
