@@ -3,7 +3,7 @@
 # and timed against the previous build: GPU tests on the product library, the traceback alone
 # (Viterbi operator under rocprofv3), then the C3 bench interleaved base / product.
 # Variants: base = tools/build_variant.sh base "" on the product source; asmld/asmld4 = the same
-# on the source with tools/tb_asm_ring.patch applied (asmld4: "-DTB_RING_N=4"); the record is
+# on the source with tools/tb_asm_ring.patch applied (asmld4: TB_RING set to 4); the record is
 # profiles/r03d_tb_asm_ab.txt.
 set -o pipefail
 O=gpurun_out/r03d; mkdir -p $O
