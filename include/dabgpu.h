@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DABGPU_ABI_VERSION 2
+#define DABGPU_ABI_VERSION 3
 
 /* error codes */
 #define DABGPU_OK          0
@@ -204,6 +204,11 @@ int dabgpu_nco_eval(dabgpu_ctx *ctx, int32_t first, int32_t n, float *out_d);
  * spectrum, which then becomes this symbol's).  spectrum_d: cf32[2048] state. */
 int dabgpu_ofdm_symbol(dabgpu_ctx *ctx, const float *samples_d, int kind, float *spectrum_d, int16_t *ibits_d);
 
+/* ofdmDecoder::get_snr (ofdm-decoder.cpp:212-230) of a T_u-point spectrum in natural
+ * bin order (cf32[2048], device): get_db(mean |X| of the signal bins) - get_db(mean |X|
+ * of the noise bins) into snr_d[0]. */
+int dabgpu_get_snr(dabgpu_ctx *ctx, const float *spectrum_d, int16_t *snr_d);
+
 /* ---- channel decoding (L4) -------------------------------------------- */
 
 /* viterbi::deconvolve batched (viterbi.cpp:225-242): n_cw codewords of
@@ -365,6 +370,15 @@ int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft_d, int32_t *ring_f
 int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot);
 /* per-frame front-end record of the last run: [n_streams][n_frames] */
 int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *frames_h, int32_t *start_index_h);
+/* The constellation display of ofdmDecoder::processToken (ofdm-decoder.cpp:192-206,
+ * displayToken 2): with on = 1 the demod keeps, for every frame it decodes, the FFT
+ * of symbol 2 at bins [0, K/2) and [T_u-1-K/2, T_u-1) -- the K values processToken
+ * pushes into iqBuffer, in that order; dabgpu_pipe_iq_display copies those of
+ * (stream, frame) of the last dabgpu_pipe_run (a decoded frame) to carriers_h[K][2].
+ * Which frames the GUI is shown (every 8th) is the caller's choice, as in the
+ * reference.  Costs 12 KB of HBM writes per frame while on. */
+int dabgpu_pipe_set_display(dabgpu_pipe *p, int on);
+int dabgpu_pipe_iq_display(dabgpu_pipe *p, int stream, int frame, float *carriers_h);
 
 #ifdef __cplusplus
 }

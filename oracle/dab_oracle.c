@@ -352,9 +352,7 @@ int16_t orc_process_block0(const float *v, float *phase_ref, int flag, int metho
     return (int16_t)(index_1 - ORC_TU);
 }
 
-void orc_process_token(const float *v, float *phase_ref, int16_t *ibits, float *softf) {   /* ofdm-decoder.cpp:167-190 */
-    tables_init();
-    float X[2 * ORC_TU];
+static void process_token_(const float *v, float *phase_ref, int16_t *ibits, float *softf, float *X) {
     orc_fft2048(v + 2 * ORC_TG, X, 0);
     for (int i = 0; i < ORC_K; i++) {
         int index = g_perm[i];
@@ -368,6 +366,11 @@ void orc_process_token(const float *v, float *phase_ref, int16_t *ibits, float *
         ibits[ORC_K + i] = (int16_t)((double)qi * 127.0);
         if (softf) { softf[i] = qr; softf[ORC_K + i] = qi; }
     }
+}
+void orc_process_token(const float *v, float *phase_ref, int16_t *ibits, float *softf) {   /* ofdm-decoder.cpp:167-190 */
+    tables_init();
+    float X[2 * ORC_TU];
+    process_token_(v, phase_ref, ibits, softf, X);
 }
 
 void orc_freqcorr(const float *v, double *acc_re, double *acc_im, float *facc) {   /* ofdm-processor.cpp:424-425 */
@@ -384,9 +387,25 @@ typedef struct {
     const float *iq; int64_t n, pos;
     int32_t localPhase; float sLevel;
     float osc_cache_re, osc_cache_im; int32_t osc_cache_i;
+    /* the spectrum feed (HAVE_SPECTRUM, ofdm-processor.cpp:161-180,220-238): sampleCnt
+     * counts the samples of every getSample / getSamples call; at the end of the call that
+     * takes it past INPUT_RATE / 7 the first 32768 raw samples read since the previous
+     * emission (localBuffer) go to spectrumBuffer */
+    int64_t spec_cnt, spec_start;
+    orc_display *disp;
 } orc_src;
 
-static int get_sample(orc_src *s, int32_t phase, cf *out) {        /* ofdm-processor.cpp:133-183 */
+static void spec_tick(orc_src *s, int n) {                          /* ofdm-processor.cpp:170-180,229-238 */
+    s->spec_cnt += n;
+    if (s->spec_cnt > ORC_INPUT_RATE / 7) {
+        if (s->disp && s->disp->n_spec < s->disp->max_spec) s->disp->spec_start[s->disp->n_spec] = s->spec_start;
+        if (s->disp) s->disp->n_spec++;
+        s->spec_cnt = 0;
+        s->spec_start = s->pos;          /* localCounter = 0: the next sample read starts the buffer */
+    }
+}
+
+static int get_sample_(orc_src *s, int32_t phase, cf *out) {
     if (s->pos >= s->n) return 0;
     cf t = {s->iq[2 * s->pos], s->iq[2 * s->pos + 1]};
     s->pos++;
@@ -402,8 +421,14 @@ static int get_sample(orc_src *s, int32_t phase, cf *out) {        /* ofdm-proce
     *out = t;
     return 1;
 }
+static int get_sample(orc_src *s, int32_t phase, cf *out) {        /* ofdm-processor.cpp:133-183 */
+    if (!get_sample_(s, phase, out)) return 0;
+    spec_tick(s, 1);
+    return 1;
+}
 static int get_samples(orc_src *s, cf *v, int n, int32_t phase) {  /* ofdm-processor.cpp:186-240 */
-    for (int i = 0; i < n; i++) if (!get_sample(s, phase, &v[i])) return 0;
+    for (int i = 0; i < n; i++) if (!get_sample_(s, phase, &v[i])) return 0;
+    spec_tick(s, n);
     return 1;
 }
 
@@ -416,7 +441,7 @@ static int get_samples(orc_src *s, cf *v, int n, int32_t phase) {  /* ofdm-proce
  * SyncOnPhase starts).  coarse + fine = 0. */
 int orc_null_scan(const float *iq, int64_t n, int scan, int32_t *attempts, int32_t *no_signal, int64_t *pos) {
     tables_init();
-    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0};
+    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0, 0, 0, NULL};
     float *envBuffer = (float *)malloc(sizeof(float) * 32768);
     const int mask = 32768 - 1;
     int idx, ret = 0;
@@ -462,22 +487,28 @@ done:
 }
 
 static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
-                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf);
-int orc_ofdm_run(const float *iq, int64_t n, int16_t threshold, int method,
-                 int max_frames, orc_frame_info *info, int16_t *softbits) {
+                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf, orc_display *disp);
+int orc_ofdm_run_display(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
+                         orc_frame_info *info, int16_t *softbits, orc_display *disp) {
     /* per call (reentrant: tests run the oracle on several streams from threads) */
     float *envBuffer = (float *)malloc(sizeof(float) * 32768);
     cf *buf = (cf *)malloc(sizeof(cf) * ORC_L * ORC_TS);
-    int ret = orc_ofdm_run_(iq, n, threshold, method, max_frames, info, softbits, envBuffer, buf);
+    if (disp) { disp->n_disp = 0; disp->n_spec = 0; }
+    int ret = orc_ofdm_run_(iq, n, threshold, method, max_frames, info, softbits, envBuffer, buf, disp);
     free(envBuffer);
     free(buf);
     return ret;
 }
+int orc_ofdm_run(const float *iq, int64_t n, int16_t threshold, int method,
+                 int max_frames, orc_frame_info *info, int16_t *softbits) {
+    return orc_ofdm_run_display(iq, n, threshold, method, max_frames, info, softbits, NULL);
+}
 
 static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
-                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf) {
+                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf, orc_display *disp) {
     tables_init();
-    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0};
+    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0, 0, 0, disp};
+    int iq_cnt = 0;                      /* processToken's static cnt (ofdm-decoder.cpp:171) */
     const int mask = 32768 - 1;
     float phase_ref[2 * ORC_TU];
     int16_t fine = 0; int32_t coarse = 0; int f2 = 1;
@@ -514,7 +545,8 @@ notSynced:
         /* SyncOnPhase :344-357 */
         int64_t wstart = s.pos;
         int32_t lpw = s.localPhase;
-        if (!get_samples(&s, buf, ORC_TU, coarse + fine)) return frames;
+        for (int i = 0; i < ORC_TU; i++)                  /* getSample, one at a time (:346-347) */
+            if (!get_sample(&s, coarse + fine, &buf[i])) return frames;
         int32_t startIndex = orc_find_index((const float *)buf, threshold, NULL, NULL);
         if (startIndex < 0) goto notSynced;
         memmove(buf, &buf[startIndex], (size_t)(ORC_TU - startIndex) * sizeof(cf));
@@ -538,8 +570,21 @@ notSynced:
             int16_t ibits[2 * ORC_K];
             if (!get_samples(&s, buf, ORC_TS, coarse + fine)) return frames;
             orc_freqcorr((const float *)buf, NULL, NULL, fc);
-            orc_process_token((const float *)buf, phase_ref, ibits, NULL);
+            float X[2 * ORC_TU];
+            process_token_(( const float *)buf, phase_ref, ibits, NULL, X);
             if (dst) memcpy(dst + (l - 1) * 2 * ORC_K, ibits, sizeof ibits);
+            /* the IQ display (ofdm-decoder.cpp:192-206): every 8th displayToken (2) the
+             * carriers fft_buffer[0, K/2) and [T_u - 1 - K/2, T_u - 1) into iqBuffer */
+            if (l == 2 && ++iq_cnt > 7) {
+                if (disp && disp->n_disp < disp->max_disp) {
+                    float *o = disp->iq_disp + (int64_t)disp->n_disp * 2 * ORC_K;
+                    memcpy(o, X, sizeof(float) * ORC_K);
+                    memcpy(o + ORC_K, X + 2 * (ORC_TU - 1 - ORC_K / 2), sizeof(float) * ORC_K);
+                    disp->disp_frame[disp->n_disp] = frames;
+                }
+                if (disp) disp->n_disp++;
+                iq_cnt = 0;
+            }
         }
         cf fcc = {fc[0], fc[1]};
         fine = (int16_t)(fine + 0.1 * carg_f(fcc) / M_PI * (ORC_CARRIER_DIFF / 2));

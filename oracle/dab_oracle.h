@@ -75,6 +75,23 @@ typedef struct {
 int     orc_null_scan(const float *iq, int64_t n, int scan, int32_t *attempts, int32_t *no_signal, int64_t *pos);
 int     orc_ofdm_run(const float *iq /*cf32[n]*/, int64_t n, int16_t threshold, int method,
                      int max_frames, orc_frame_info *info, int16_t *softbits /*[max_frames][75][3072]*/);
+/* ... and the two display feeds of the reference's OFDM classes:
+ *   iqBuffer (ofdmDecoder::processToken, ofdm-decoder.cpp:192-206): every 8th call with
+ *     blkno == displayToken (2), fft_buffer[0, K/2) then [T_u-1-K/2, T_u-1): iq_disp[k]
+ *     holds K cf32 values, disp_frame[k] the frame they came from;
+ *   spectrumBuffer (ofdmProcessor::getSample(s), ofdm-processor.cpp:161-180,220-238):
+ *     spec_start[k] = stream index of the first of the 32768 raw (pre-NCO) samples of
+ *     the k-th emission.
+ * n_disp / n_spec count every emission (entries past max_* are not stored). */
+typedef struct {
+    float   *iq_disp;       /* [max_disp][K][2] */
+    int32_t *disp_frame;    /* [max_disp] */
+    int32_t  max_disp, n_disp;
+    int64_t *spec_start;    /* [max_spec] */
+    int32_t  max_spec, n_spec;
+} orc_display;
+int     orc_ofdm_run_display(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
+                             orc_frame_info *info, int16_t *softbits, orc_display *disp);
 
 /* ---- backend ---- */
 void    orc_viterbi(const int16_t *in /*[4*(nbits+6)]*/, int nbits, uint8_t *out /*[nbits]*/); /* viterbi.cpp:225-242 */

@@ -34,8 +34,8 @@ __device__ __forceinline__ float2 cmul_conj_exact(float2 a, float2 b) {   // a *
     float ac = a.x * b.x, bd = a.y * nb, ad = a.x * nb, bc = a.y * b.x;
     return make_float2(ac - bd, ad + bc);
 }
-// oscillatorTable[t] from the factor tables (dab_kernels.h, NCO_*), bit-exact
-__device__ __forceinline__ float2 nco_value(const double2 *tab, int32_t t) {
+// e^{2 pi i t / 2048000} in double from the factor tables (dab_kernels.h, NCO_*)
+__device__ __forceinline__ double2 nco_value_d(const double2 *tab, int32_t t) {
 #pragma clang fp contract(off)
     const uint32_t a = (uint32_t)t / 16000u;
     const uint32_t r = (uint32_t)t - a * 16000u;
@@ -44,7 +44,12 @@ __device__ __forceinline__ float2 nco_value(const double2 *tab, int32_t t) {
     const double pi = __builtin_fma(B.x, C.y, B.y * C.x);
     const double vr = __builtin_fma(A.x, pr, -(A.y * pi));
     const double vi = __builtin_fma(A.x, pi, A.y * pr);
-    return make_float2((float)vr, (float)vi);
+    return make_double2(vr, vi);
+}
+// oscillatorTable[t], bit-exact: the double value rounded to float
+__device__ __forceinline__ float2 nco_value(const double2 *tab, int32_t t) {
+    const double2 v = nco_value_d(tab, t);
+    return make_float2((float)v.x, (float)v.y);
 }
 // FFT-internal product (fused is fine inside the transform)
 __device__ __forceinline__ float2 cmul(float2 a, float wr, float wi) {

@@ -37,6 +37,9 @@ struct DemodAux {
     float *maxv, *sumv;     // optional: findIndex's Max and sum |r|
     int16_t *snr;           // optional: get_snr of block 0 per frame
     int32_t level;          // findIndex threshold
+    float2 *disp;           // optional: [out_slot][K] symbol 2's FFT at bins [0, K/2) and
+                            // [T_u-1-K/2, T_u-1) -- the iqBuffer feed of processToken
+                            // (ofdm-decoder.cpp:192-206)
 };
 constexpr int KERR_FRAME = 1;      // frame descriptor outside its stream / bad NCO phase
 constexpr int KERR_VITERBI = 2;    // Viterbi source outside its buffer
@@ -159,6 +162,7 @@ hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
                         const DemodAux &aux);
 hipError_t launch_nco_eval(hipStream_t st, const OfdmTables &T, int32_t first, int32_t n, float2 *out);
+hipError_t launch_snr(hipStream_t st, const float *spec, int16_t *out);
 hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmTables &T, float *spec, int16_t *ibits);
 hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int n, float *out);
 hipError_t launch_take_error(hipStream_t st, int32_t *err, int32_t *h_err);

@@ -585,6 +585,11 @@ int dabgpu_ofdm_symbol(dabgpu_ctx *c, const float *smp, int kind, float *spec, i
     HIPCHK(launch_symbol(c->stream, smp, kind, c->T, spec, ibits));
     return 0;
 }
+int dabgpu_get_snr(dabgpu_ctx *c, const float *spectrum, int16_t *snr) {
+    if (!c || !spectrum || !snr) return fail(DABGPU_E_ARG, "bad args");
+    HIPCHK(launch_snr(c->stream, spectrum, snr));
+    return 0;
+}
 int dabgpu_nco_eval(dabgpu_ctx *c, int32_t first, int32_t n, float *out) {
     if (!c || !out || first < 0 || n < 0 || (int64_t)first + n > M) return fail(DABGPU_E_ARG, "bad args");
     if (n) HIPCHK(launch_nco_eval(c->stream, c->T, first, n, (float2 *)out));
@@ -835,6 +840,9 @@ struct dabgpu_pipe {
     int64_t run_idx = 0;
     Profile *ficprof_d = nullptr;
     uint16_t *inv_d = nullptr;       // the subchannel profiles' inverse depuncturing tables
+    // the iqBuffer feed (dabgpu_pipe_set_display): symbol 2's display carriers per ring slot
+    float2 *disp_d = nullptr;        // [S][R][K]
+    bool display = false;
     // optional per-stage kernel timing (HIP events on the stage's stream)
     int profiling = 0;                          // 1: last run, 2: every run since enabled, 3: 2 + stages alone
     std::vector<hipEvent_t> ev_pool;
@@ -1053,7 +1061,7 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->cif0_d, (void *)p->ncif_d, (void *)p->berr_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d,
-                    (void *)p->dp_cand_d})
+                    (void *)p->dp_cand_d, (void *)p->disp_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
@@ -1207,6 +1215,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         aux.si = p->si_d;
         aux.snr = p->snr_d;
         aux.level = p->threshold;
+        aux.disp = p->display ? p->disp_d : nullptr;
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         const int kChunks = demod_chunks(n, 2);
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
@@ -1326,6 +1335,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         const int kChunks = demod_chunks(n3);
         DemodAux aux{};
+        aux.disp = p->display ? p->disp_d : nullptr;
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
@@ -1751,6 +1761,29 @@ int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft, int32_t *ring) {
 int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot) {
     if (!p || !slot || frame < 0 || frame >= p->F) return fail(DABGPU_E_ARG, "bad args");
     *slot = p->last_frames.empty() ? -1 : p->last_frames[frame].out_slot;
+    return 0;
+}
+int dabgpu_pipe_set_display(dabgpu_pipe *p, int on) {
+    if (!p) return fail(DABGPU_E_ARG, "bad args");
+    if (on && !p->disp_d) {
+        HIPCHK(hipStreamSynchronize(p->c->stream));
+        HIPCHK(hipMalloc((void **)&p->disp_d, sizeof(float2) * (size_t)p->S * p->R * K));
+        HIPCHK(hipMemset(p->disp_d, 0, sizeof(float2) * (size_t)p->S * p->R * K));
+    }
+    p->display = on != 0;
+    return 0;
+}
+int dabgpu_pipe_iq_display(dabgpu_pipe *p, int stream, int frame, float *carriers_h) {
+    if (!p || !carriers_h || stream < 0 || stream >= p->S || frame < 0 || frame >= p->F)
+        return fail(DABGPU_E_ARG, "bad args");
+    if (!p->display || !p->disp_d) return fail(DABGPU_E_STATE, "display feed off (dabgpu_pipe_set_display)");
+    const size_t i = (size_t)stream * p->F + frame;
+    if (p->last_info.size() <= i || !p->last_info[i].committed)
+        return fail(DABGPU_E_STATE, "stream %d frame %d was not decoded in the last run", stream, frame);
+    const int32_t slot = p->last_frames[i].out_slot;
+    HIPCHK(hipMemcpyAsync(carriers_h, p->disp_d + (size_t)slot * K, sizeof(float2) * K, hipMemcpyDeviceToHost,
+                          p->c->stream));
+    HIPCHK(hipStreamSynchronize(p->c->stream));
     return 0;
 }
 int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *fr, int32_t *si) {

@@ -453,18 +453,39 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         __syncthreads();                                // pass 3 read ex: the first symbol's pass 1 writes it
 #pragma unroll
         for (int k = 0; k < 8; k++) P[k] = a[k];
-        // NCO of segment B: localPhase index of this thread's sample 0 of symbol l, stepped
-        // in 32 bits (-256 phase per register, -T_s phase per symbol, +512/+256 phase for
-        // the two guard samples); phase 0: oscillatorTable[lp_data] for every sample.  The
-        // three separately branched mixes keep the NCO's doubles out of the FFT's
-        // scheduling region (one region: the register allocator spills)
+        // NCO of segment B (round 4): thread t's samples of symbol l are n = t + 256 m, so
+        // their oscillatorTable indices step by -d256 per m and by -dsym per symbol (mod
+        // 2048000).  The exact e^{2 pi i ti / N} of the chunk's first sample (the factor
+        // tables, in double) then follows the index by complex double recurrences
+        // -- x R = e^{-2 pi i d256 / N} per sample, x D = e^{-2 pi i dsym / N} per symbol,
+        // both wave-uniform SGPR pairs -- rounded to float per sample: the table's value
+        // (its float rounding of the same double) except within ~1e-13 of a rounding
+        // boundary, as the relative error of the double recurrence grows by ~2^-53 per
+        // step.  The per-sample table rebuild cost 28 VALU + 3 conflicted LDS gathers per
+        // sample; this is 6 f64 ops.  Phase 0: oscillatorTable[lp_data].
         const float2 f0 = T.osc[fr.lp_data];
         const int32_t ph = fr.phase_b;
-        // wave-uniform steps: SGPRs (readfirstlane), no VGPRs taken from the FFT
-        const int32_t d256 = __builtin_amdgcn_readfirstlane(nco_mod(256 * (int64_t)ph));
-        const int32_t dsym = __builtin_amdgcn_readfirstlane(nco_mod((int64_t)TS * ph));
-        const int32_t g512 = __builtin_amdgcn_readfirstlane(nco_mod(512 * (int64_t)ph)), g256 = d256;
-        int32_t ti = nco_index2(fr.lp_data, ph, fr.block0 + (int64_t)l0 * TS + t - dorg + 1);
+        auto uni = [](double v) {               // wave-uniform double -> SGPR pair
+            const uint64_t b = __builtin_bit_cast(uint64_t, v);
+            const uint64_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)b);
+            const uint64_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+            return __builtin_bit_cast(double, lo | (hi << 32));
+        };
+        auto cmul_d = [](double2 x, double yr, double yi) {
+            return make_double2(__builtin_fma(x.x, yr, -(x.y * yi)), __builtin_fma(x.x, yi, x.y * yr));
+        };
+        double2 w = make_double2(1.0, 0.0);     // e^{2 pi i ti / N}, ti: this thread's sample 0 of symbol l
+        double rr = 1.0, ri = 0.0, dr = 1.0, di = 0.0;
+        float2 efc = make_float2(1.0f, 0.0f);   // FreqCorr of mixed samples = raw x oscillatorTable[-T_u phase]
+        if (GEN && ph != 0) {
+            const int32_t d256 = nco_mod(256 * (int64_t)ph), dsym = nco_mod((int64_t)TS * ph);
+            w = nco_value_d(ncl, nco_index2(fr.lp_data, ph, fr.block0 + (int64_t)l0 * TS + t - dorg + 1));
+            const double2 r = nco_value_d(ncl, nco_mod(-(int64_t)d256));
+            const double2 d = nco_value_d(ncl, nco_mod(-(int64_t)dsym));
+            rr = uni(r.x); ri = uni(r.y);
+            dr = uni(d.x); di = uni(d.y);
+            efc = nco_value(ncl, nco_mod(-(int64_t)TU * ph));
+        }
         for (int l = l0; l < l1; l++) {
             // this symbol's samples and its guard samples, all loaded one symbol ahead
             // (a guard load issued here would expose a full HBM latency per symbol)
@@ -479,23 +500,10 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 for (int m = 0; m < 8; m++) nx[m] = ld(o1 + 2048 * m);
             }
             ov += TS * 8;
-            if (!GEN || ph == 0) {
-#pragma unroll
-                for (int m = 0; m < 8; m++) a[m] = cmul_exact(a[m], f0);
-            } else {
-                int32_t x = ti;
-#pragma unroll
-                for (int m = 0; m < 8; m++) {
-                    a[m] = cmul_exact(a[m], nco_value(ncl, x));
-                    x = nco_sub(x, d256);
-                }
-            }
-            if (!GEN || ph == 0) g6 = cmul_exact(g6, f0);
-            else g6 = cmul_exact(g6, nco_value(ncl, nco_add(ti, g512)));
-            if (!GEN || ph == 0) g7 = cmul_exact(g7, f0);
-            else g7 = cmul_exact(g7, nco_value(ncl, nco_add(ti, g256)));
-            ti = nco_sub(ti, dsym);
-            if (t >= 8) {                              // FreqCorr over i in [T_u, T_s)
+            // FreqCorr over i in [T_u, T_s) on the samples before the NCO: the mixed
+            // product x[i] conj(x[i - T_u]) is the raw one times oscillatorTable[-T_u phase]
+            // (efc, applied once at the end)
+            if (t >= 8) {
                 const float2 p = cmul_conj_exact(a[6], g6);
                 fc.x += p.x; fc.y += p.y;
             }
@@ -503,7 +511,29 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 const float2 p = cmul_conj_exact(a[7], g7);
                 fc.x += p.x; fc.y += p.y;
             }
+            if (!GEN || ph == 0) {
+#pragma unroll
+                for (int m = 0; m < 8; m++) a[m] = cmul_exact(a[m], f0);
+            } else {
+                double2 v = w;
+#pragma unroll
+                for (int m = 0; m < 8; m++) {
+                    a[m] = cmul_exact(a[m], make_float2((float)v.x, (float)v.y));
+                    if (m < 7) v = cmul_d(v, rr, ri);
+                }
+                w = cmul_d(w, dr, di);
+            }
             fft2048_wg(a, ex, tw, t);
+            if (l == 2 && aux.disp) {                  // the display token's carriers (ofdm-decoder.cpp:197-205)
+                float2 *dp = aux.disp + (int64_t)fr.out_slot * K;
+                const int b0 = bin0_of(t);
+#pragma unroll
+                for (int k = 0; k < 8; k++) {
+                    const int b = b0 + 64 * k;
+                    if (b < K / 2) dp[b] = a[k];
+                    else if (b >= TU - 1 - K / 2 && b < TU - 1) dp[b - (TU - 1 - K)] = a[k];
+                }
+            }
             __syncthreads();                           // pass 3's reads of ex done: st reuses it
             // DQPSK + soft bits of the 8 bins, fast path first; the few bins whose
             // truncation the fast path cannot decide (soft_fast) are redone exactly after
@@ -562,6 +592,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             }
             __syncthreads();
         }
+        fc = cmulw(fc, efc);
     }
     fc.x = wave_sum(fc.x);
     fc.y = wave_sum(fc.y);
@@ -753,6 +784,22 @@ __global__ __launch_bounds__(DT) void k_symbol_wg(const float2 *__restrict__ smp
         }
         spec[b] = a[k];
     }
+}
+
+// get_snr (ofdm-decoder.cpp:212-230) of a spectrum in natural bin order: the
+// ofdmDecoder::get_snr drop-in, the same workgroup reduction as the fused kernels'
+__global__ __launch_bounds__(DT) void k_snr_wg(const float2 *__restrict__ spec, int16_t *__restrict__ out) {
+    __shared__ RedLds red;
+    const int t = threadIdx.x, b0 = bin0_of(t);
+    float2 a[8];
+#pragma unroll
+    for (int k = 0; k < 8; k++) a[k] = spec[b0 + 64 * k];
+    const int16_t v = snr_wg(a, t, red);
+    if (t == 0) *out = v;
+}
+hipError_t launch_snr(hipStream_t st, const float *spec, int16_t *out) {
+    hipLaunchKernelGGL(k_snr_wg, dim3(1), dim3(DT), 0, st, (const float2 *)spec, out);
+    return hipGetLastError();
 }
 
 // the kernels' NCO over a range of table indices (exhaustive parity check)

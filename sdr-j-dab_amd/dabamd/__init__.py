@@ -96,6 +96,7 @@ def lib() -> C.CDLL:
             "dabgpu_memset_d": ([vp, vp, i32, sz], i32),
             "dabgpu_memcpy_d2d": ([vp, vp, vp, sz], i32),
             "dabgpu_ofdm_symbol": ([vp, vp, i32, vp, vp], i32),
+            "dabgpu_get_snr": ([vp, vp, vp], i32),
             "dabgpu_nco_eval": ([vp, i32, i32, vp], i32),
             "dabgpu_iq_convert": ([vp, i32, vp, i64, vp], i32),
             "dabgpu_event_record": ([vp, i32], i32),
@@ -121,6 +122,8 @@ def lib() -> C.CDLL:
             "dabgpu_pipe_softbits": ([vp, C.POINTER(vp), C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frame_slot": ([vp, i32, C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frames": ([vp, vp, vp], i32),
+            "dabgpu_pipe_set_display": ([vp, i32], i32),
+            "dabgpu_pipe_iq_display": ([vp, i32, i32, vp], i32),
             "dabgpu_pipe_set_profiling": ([vp, i32], i32),
             "dabgpu_pipe_timing": ([vp, vp, vp], i32),
         }
@@ -584,6 +587,17 @@ class Pipeline:
         si = np.zeros(n, dtype=np.int32)
         _chk(lib().dabgpu_pipe_frames(self.h, C.cast(fr, C.c_void_p), _p(si)), "dabgpu_pipe_frames")
         return list(fr), si.reshape(self.S, self.F)
+
+    def set_display(self, on: bool = True) -> None:
+        """keep symbol 2's display carriers of every decoded frame (dabgpu_pipe_set_display)"""
+        _chk(lib().dabgpu_pipe_set_display(self.h, int(on)), "dabgpu_pipe_set_display")
+
+    def iq_display(self, stream: int, frame: int) -> np.ndarray:
+        """processToken's iqBuffer values (ofdm-decoder.cpp:197-205) of (stream, frame) of
+        the last run: complex64 [1536]"""
+        out = np.zeros((K, 2), np.float32)
+        _chk(lib().dabgpu_pipe_iq_display(self.h, stream, frame, _p(out)), "dabgpu_pipe_iq_display")
+        return out[:, 0] + 1j * out[:, 1]
 
     def softbits(self) -> np.ndarray:
         """the soft-bit ring of the last run as [stream][slot][75][3072] ibits rows"""

@@ -30,6 +30,7 @@
 #include "dabgpu.h"
 #include "fib_processor.h"
 #include "msc_consumers.h"
+#include "ringbuffer.h"
 
 namespace dabgpu {
 
@@ -294,33 +295,74 @@ private:
     int16_t new_language_ = 0, new_type_ = 0;
 };
 
+// ---- libsndfile stand-in (the .sdr dump) ---------------------------------------------
+// gui.cpp:861-893 opens the dump with sf_open (path, SFM_WRITE, {INPUT_RATE, 2 channels,
+// SF_FORMAT_WAV | SF_FORMAT_PCM_16}) and hands the SNDFILE* to ofdmProcessor::startDumping,
+// which writes interleaved PCM16 frames with sf_writef_short (ofdm-processor.cpp:150-157).
+// libsndfile is not in this image: this is the subset those calls use, writing the same
+// RIFF/WAVE PCM16 file (the header's sizes are filled in by sf_close).
+struct SF_INFO {
+    int64_t frames;
+    int samplerate, channels, format, sections, seekable;
+};
+struct SNDFILE;
+constexpr int SFM_WRITE = 0x20;
+constexpr int SF_FORMAT_WAV = 0x010000, SF_FORMAT_PCM_16 = 0x0002;
+SNDFILE *sf_open(const char *path, int mode, SF_INFO *info);   // SFM_WRITE, WAV PCM16 only (else nullptr)
+int64_t sf_writef_short(SNDFILE *f, const int16_t *ptr, int64_t frames);
+int sf_close(SNDFILE *f);
+
 // ---- OFDM front end ----------------------------------------------------------------
-// ofdmDecoder (ofdm-decoder.cpp:85-230) one symbol per call on the GPU: processBlock_0
-// = get_snr (IIR 0.7/0.3, show_snr every 11 blocks) + coarse offset of freqSyncMethod
-// 0/1/2 + the spectrum as phase reference; processToken = FFT + DQPSK + frequency
-// de-interleave -> 3072 soft bits.  Samples are the caller's, already NCO-mixed.
+// ofdmDecoder (ofdm-decoder.cpp:37-230, ofdm-decoder.h:40-48) one symbol per call on the
+// GPU: processBlock_0 = get_snr (IIR 0.7/0.3, show_snr every 11 blocks) + coarse offset of
+// freqSyncMethod 0/1/2 + the spectrum as phase reference; processToken = FFT + DQPSK +
+// frequency de-interleave -> 3072 soft bits, and every 8th displayToken (blkno 2) the
+// carriers fft_buffer[0, K/2) and [T_u-1-K/2, T_u-1) into iqBuffer + showIQ(K)
+// (ofdm-decoder.cpp:192-206; the counter is shared by every decoder, as the reference's
+// function-static cnt).  Samples are the caller's, already NCO-mixed.  The reference's
+// RadioInterface* is the signals struct; refTable (phaseReference::getTable) only feeds
+// refArg (ofdm-decoder.cpp:71-74), which the device tables hold already.
 class ofdmDecoder {
 public:
+    struct signals {
+        std::function<void(int)> show_snr, showIQ;
+    };
+    ofdmDecoder(DabParams *p, RingBuffer<DSPCOMPLEX> *iqBuffer, DSPCOMPLEX *refTable, signals sig,
+                uint8_t freqSyncMethod);
     ofdmDecoder(DabParams *p, uint8_t freqSyncMethod = 1, std::function<void(int)> show_snr = nullptr);
     int16_t processBlock_0(DSPCOMPLEX *vi, bool flag);
     void processToken(DSPCOMPLEX *inv, int16_t *ibits, int32_t blkno);
+    // get_snr (ofdm-decoder.cpp:212-230) of a T_u-point spectrum (natural bin order)
+    int16_t get_snr(DSPCOMPLEX *v);
     int16_t snr() const { return snr_; }
+    // processToken's `static int cnt` (ofdm-decoder.cpp:171): one count per process
+    static std::atomic<int> iq_count;
+    static constexpr int16_t displayToken = 2;                 // ofdm-decoder.cpp:63
 private:
     uint8_t method_;
-    std::function<void(int)> show_snr_;
+    RingBuffer<DSPCOMPLEX> *iqBuffer_ = nullptr;
+    signals sig_;
     int16_t snr_ = 0, snrCount_ = 0;
     devbuf smp_, spec_, fr_, corr_, snrd_, bits_;
 };
 
-// ofdmProcessor (ofdm-processor.cpp:34-509): the constructor starts the thread that pulls
-// samples from the virtualInput into a sliding window in HBM and runs the GPU front end
-// (the dabgpu_pipe_* engine for one stream: null search, findIndex, coarse/fine AFC,
-// demod); every decoded frame's symbols go to ficHandler::process_ficBlock (blkno
-// 1..3) and mscHandler::process_mscBlock (4..75) with the reference's soft bits.  The
-// GUI signals are callbacks: show_fineCorrector / show_coarseCorrector (every
-// INPUT_RATE/7 samples, at frame granularity), show_avgTokenLength (every 11 frames),
-// setSynced, No_Signal_Found (scan mode) and show_snr.  startDumping writes the raw
-// samples as interleaved PCM16 (the .sdr payload) with the reference's scaling.
+// ofdmProcessor (ofdm-processor.cpp:34-509, ofdm-processor.h:49-59): the constructor
+// starts the thread that pulls samples from the virtualInput into a sliding window in
+// HBM and runs the GPU front end (the dabgpu_pipe_* engine for one stream: null search,
+// findIndex, coarse/fine AFC, demod); every decoded frame's symbols go to
+// ficHandler::process_ficBlock (blkno 1..3) and mscHandler::process_mscBlock (4..75) with
+// the reference's soft bits.  The GUI signals are callbacks (the RadioInterface* of the
+// reference): show_avgTokenLength (every 11 frames), setSynced, No_Signal_Found (scan
+// mode), show_snr, and at the reference's sample positions -- the end of the getSample /
+// getSamples call that takes the sample count past INPUT_RATE/7, replayed from the
+// frames the GPU decoded -- show_fineCorrector / show_coarseCorrector and, with a
+// spectrumBuffer (HAVE_SPECTRUM), the 32768 raw samples read since the previous one
+// into the ring + showSpectrum(32768) (ofdm-processor.cpp:161-180,220-238).  With an
+// iqBuffer every 8th frame's symbol-2 carriers go into it + showIQ(K), as the
+// reference's ofdmDecoder does (ofdm-decoder.cpp:192-206; the GPU demod exports them,
+// dabgpu_pipe_iq_display).  startDumping writes the raw samples as interleaved PCM16
+// (the .sdr payload, ofdm-processor.cpp:150-157) with the reference's scaling, through
+// sf_writef_short (SNDFILE*) or as bare PCM16 into a FILE*.
 class ficHandler;
 class ofdmProcessor {
 public:
@@ -328,7 +370,13 @@ public:
         std::function<void(int)> show_fineCorrector, show_coarseCorrector, show_avgTokenLength, show_snr;
         std::function<void(char)> setSynced;
         std::function<void()> No_Signal_Found;
+        std::function<void(int)> showSpectrum, showIQ;
     };
+    // the reference's argument list (spectrumBuffer: HAVE_SPECTRUM builds; either ring may be null)
+    ofdmProcessor(virtualInput *theRig, DabParams *p, signals sig, mscHandler *msc, ficHandler *fic,
+                  int16_t threshold, RingBuffer<DSPCOMPLEX> *spectrumBuffer, RingBuffer<DSPCOMPLEX> *iqBuffer,
+                  uint8_t freqSyncMethod);
+    // without display rings (a build without HAVE_SPECTRUM and no IQ scope)
     ofdmProcessor(virtualInput *theRig, DabParams *p, signals sig, mscHandler *msc, ficHandler *fic,
                   int16_t threshold = 3, uint8_t freqSyncMethod = 1);
     ~ofdmProcessor();
@@ -337,31 +385,48 @@ public:
     void coarseCorrectorOn();
     void coarseCorrectorOff();
     void set_scanMode(bool b);
+    void startDumping(SNDFILE *f);
     void startDumping(FILE *f);
     void stopDumping();
     int64_t frames() const { return frames_.load(); }
+    static constexpr int32_t spectrumSize = 32768;          // bufferSize (ofdm-processor.cpp:97)
 private:
     void run();
     void emit_frame(const dabgpu_frame_info &fi);
+    // the reference's getSample / getSamples calls, replayed for the spectrum feed
+    void consume_singles(int64_t to, const dabgpu_frame_info *fi);
+    void consume_block(int64_t n, const dabgpu_frame_info *fi);
+    void spectrum_emit(const dabgpu_frame_info *fi);
+    void write_dump(const DSPCOMPLEX *v, int32_t n);
     virtualInput *theRig_;
     signals sig_;
     mscHandler *msc_;
     ficHandler *fic_;
     int16_t threshold_;
     uint8_t method_;
+    RingBuffer<DSPCOMPLEX> *spectrumBuffer_ = nullptr, *iqBuffer_ = nullptr;
     std::thread thread_;
     std::atomic<bool> running_{false};
     std::atomic<int64_t> frames_{0};
     std::mutex ctl_;
     std::vector<int> pending_ops_;
     std::atomic<FILE *> dumpFile_{nullptr};
+    std::atomic<SNDFILE *> dumpSnd_{nullptr};
     int16_t dumpScaler_ = 512;
     // observables state
-    int64_t sampleCnt_ = 0, last_block0_ = -1, prev_window_ = -1;
+    int64_t last_block0_ = -1;
     int32_t avgTokenLength_ = 196608, tokenCount_ = 0;
     int16_t snr_ = 0, snrCount_ = 0;
     int32_t no_signal_ = 0, resyncs_ = 0;
     bool synced_ = false;
+    // spectrum feed replay: samples consumed, sampleCnt, first sample of localBuffer
+    int64_t consumed_ = 0, spec_cnt_ = 0, spec_start_ = 0;
+    int16_t last_fine_ = 0;
+    int32_t last_coarse_ = 0;
+    // the device sample window (run()): the spectrum block is read back from it
+    const float *win_ = nullptr;
+    int64_t win_base_ = 0;
+    std::vector<DSPCOMPLEX> specbuf_;
 };
 
 // The streaming engine: ofdmProcessor::run + ficHandler + mscHandler (+ DAB+

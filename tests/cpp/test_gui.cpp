@@ -232,8 +232,32 @@ int main(int argc, char **argv) {
             msch.set_dataChannel(&pd);
         }
         int64_t frames = 0;
+        // the GUI's display rings (gui.cpp:109,123) and their readers: showIQ takes `amount`
+        // values (gui.cpp:1223-1229), showSpectrum the spectrum handler's block and flushes
+        // (spectrum-handler.cpp:113-125; here the whole 32768 samples)
+        dabgpu::RingBuffer<dabgpu::DSPCOMPLEX> iqBuffer(2 * 1536), spectrumBuffer(2 * 32768);
+        std::vector<dabgpu::DSPCOMPLEX> iqv, specv;
+        int n_iq = 0, n_spec = 0, iq_short = 0;
+        dabgpu::ofdmProcessor::signals os;
+        os.showIQ = [&](int amount) {
+            std::vector<dabgpu::DSPCOMPLEX> Values(amount);
+            const int t = iqBuffer.getDataFromBuffer(Values.data(), amount);
+            iq_short += t != amount;
+            iqv.insert(iqv.end(), Values.begin(), Values.begin() + t);
+            n_iq++;
+        };
+        os.showSpectrum = [&](int amount) {
+            if (spectrumBuffer.GetRingBufferReadAvailable() < amount) return;
+            std::vector<dabgpu::DSPCOMPLEX> sp(amount);
+            spectrumBuffer.getDataFromBuffer(sp.data(), amount);
+            spectrumBuffer.FlushRingBuffer();
+            specv.insert(specv.end(), sp.begin(), sp.end());
+            n_spec++;
+        };
+        dabgpu::ofdmDecoder::iq_count = 0;          // a fresh GUI process: processToken's static cnt is 0
         {
-            dabgpu::ofdmProcessor ofdm(&input, &p, dabgpu::ofdmProcessor::signals{}, &msch, &fic, 3, 1);
+            dabgpu::ofdmProcessor ofdm(&input, &p, kind == 0 ? os : dabgpu::ofdmProcessor::signals{}, &msch, &fic, 3,
+                                       kind == 0 ? &spectrumBuffer : nullptr, kind == 0 ? &iqBuffer : nullptr, 1);
             CHECK(wait_for([&] { return ofdm.frames() >= NF; }, 60), "part B frames %lld", (long long)ofdm.frames());
             std::this_thread::sleep_for(std::chrono::milliseconds(100));
             frames = ofdm.frames();
@@ -248,6 +272,20 @@ int main(int argc, char **argv) {
         std::fclose(f);
         std::printf("part B %s: %lld frames, %zu data groups\n", kind == 0 ? "mp2" : "packet", (long long)frames,
                     groups.size());
+        if (kind == 0) {
+            // the display feeds, compared with the oracle's by tests/test_gpu_dropin.py
+            CHECK(n_iq >= 2 && iq_short == 0, "showIQ %d times (%d short reads)", n_iq, iq_short);
+            CHECK(n_spec >= 10, "showSpectrum %d times", n_spec);
+            for (auto [name, v] : {std::make_pair("/iq_display.bin", &iqv), std::make_pair("/spectrum.bin", &specv)}) {
+                FILE *o = std::fopen((outdir + name).c_str(), "wb");
+                CHECK(o != nullptr, "open %s", name);
+                if (o) {
+                    std::fwrite(v->data(), sizeof(dabgpu::DSPCOMPLEX), v->size(), o);
+                    std::fclose(o);
+                }
+            }
+            std::printf("display feeds: showIQ %d x 1536 carriers, showSpectrum %d x 32768 samples\n", n_iq, n_spec);
+        }
     }
     if (failures) {
         std::printf("GUI FAILED (%d)\n", failures);

@@ -68,6 +68,25 @@ def test_gui_sequence_and_msc_consumers_match_oracle(tmp_path):
     assert d.crc_errors == 0 and len(d.groups) >= 10
     assert groups[:len(d.groups)] == d.groups
     assert len(groups) - len(d.groups) <= 16
+    # the OFDM classes' display feeds (ofdm-processor.h:49-59, ofdm-decoder.h:40-44):
+    # iqBuffer (ofdm-decoder.cpp:192-206) -- every 8th frame's symbol-2 carriers, within
+    # 1e-5 of the spectrum's RMS of the oracle's FFT of the same (NCO-mixed) samples;
+    # spectrumBuffer (ofdm-processor.cpp:161-180,220-238) -- 32768 raw input samples per
+    # emission, at the reference's positions, bit for bit
+    _, _, _, disp, dfr, spec = orc.ofdm_run_display(g["iq"], NF + 1, max_disp=16, max_spec=64)
+    iqd = np.fromfile(tmp_path / "iq_display.bin", np.complex64).reshape(-1, 1536)
+    k = min(len(iqd), len(disp))
+    assert k >= 3 and list(dfr[:3]) == [7, 15, 23]
+    for i in range(k):
+        rms = np.sqrt(np.mean(np.abs(disp[i]) ** 2))
+        err = np.abs(iqd[i] - disp[i]).max() / rms
+        assert err <= 1e-5, (i, err)
+    spd = np.fromfile(tmp_path / "spectrum.bin", np.complex64).reshape(-1, 32768)
+    x = g["iq"].view(np.complex64)
+    k = min(len(spd), len(spec))
+    assert k >= 10 and len(spec) - len(spd) <= 2, (len(spd), len(spec))
+    for i in range(k):
+        assert np.array_equal(spd[i].view(np.uint64), x[spec[i]:spec[i] + 32768].view(np.uint64)), (i, spec[i])
 
 
 def test_cpp_dropin_builds():

@@ -263,6 +263,68 @@ def test_demod_matches_oracle(ctx, synth_stream):
     iq.free()
 
 
+def _nco_mix(x, pos, lp, phase, origin, osc):
+    """getSamples' NCO (ofdm-processor.cpp:186-201) on samples at absolute positions pos
+    of a segment starting at origin: v *= oscillatorTable[(lp - (p - origin + 1) phase) mod
+    2048000], as std::complex<float> (each product rounded, then the sum)"""
+    idx = (lp - (pos - origin + 1).astype(np.int64) * phase) % 2048000
+    o = osc[idx]
+    xr, xi = x[:, 0], x[:, 1]
+    re = (xr * o[:, 0]).astype(np.float32) - (xi * o[:, 1]).astype(np.float32)
+    im = (xr * o[:, 1]).astype(np.float32) + (xi * o[:, 0]).astype(np.float32)
+    return np.stack([re, im], axis=1).astype(np.float32)
+
+
+@pytest.mark.parametrize("phase", [1300, -4201, 517])
+def test_demod_nco_matches_oracle(ctx, synth_stream, phase):
+    """processToken under a carrier offset (the per-sample NCO of getSamples): the GPU
+    demod's float soft values (its NCO: the exact e^{2 pi i t/N} of the chunk's first
+    sample followed by double recurrences, rounded per sample) within 1e-5 of the
+    oracle's on the reference-mixed samples; int16 soft bits equal except at rounding
+    boundaries; FreqCorr (ofdm-processor.cpp:424-438) within 1e-3.  (A 12.3 kHz NCO on
+    this 0 Hz stream smears carriers into near-empty bins whose q the fp32 FFT's rounding
+    moves by 5.4e-5 -- with the round-3 per-sample exact table too: the FFT's floor, not
+    the NCO's; profiles/r04_nco_ab.txt.)"""
+    import dabamd
+    g, info, _ = synth_stream
+    osc = dabamd.host_table(dabamd.TABLE_OSC)
+    x = g["iq"].reshape(-1, 2)
+    iq = ctx.put(g["iq"])
+    frs = []
+    for i, fi in enumerate(info):
+        w = fi.window_start
+        b0 = w + fi.start_index
+        frs.append(dabamd.Frame(iq_base=0, n_samples=len(x), window=w, block0=b0, out_slot=i, flags=1,
+                                lp_window=(777 * i + 1000003) % 2048000, phase_a=phase,
+                                lp_data=(31337 * i + 5) % 2048000, phase_b=phase + 17))
+    soft, softf, fc = ctx.demod(iq, frs, with_float=True)
+    for i, fr in enumerate(frs):
+        pa = np.arange(fr.block0, fr.block0 + 2048)
+        blk = _nco_mix(x[pa], pa, fr.lp_window, fr.phase_a, fr.window, osc)
+        _, pr = orc.process_block0(blk.reshape(-1), flag=0)
+        dorg = fr.block0 + 2048
+        pb = np.arange(dorg, dorg + 75 * 2552)
+        seg = _nco_mix(x[pb], pb, fr.lp_data, fr.phase_b, dorg, osc)
+        fc_ref = 0j
+        worst = 0.0
+        for l in range(1, 76):
+            sym = seg[(l - 1) * 2552:l * 2552]
+            ib, sf = orc.process_token(sym.reshape(-1), pr)
+            d = np.abs(softf[i, l - 1] - sf)
+            worst = max(worst, float(d.max()))
+            bad = ib != soft[i, l - 1]
+            if bad.any():
+                q = sf[bad].astype(np.float64) * 127.0
+                assert np.all(np.abs(q - np.round(q)) < 2e-3), (phase, i, l, q[:5])
+                assert np.all(np.abs(ib[bad].astype(int) - soft[i, l - 1][bad]) <= 1)
+            c = sym[:, 0].astype(np.float64) + 1j * sym[:, 1]
+            fc_ref += np.sum(c[2048:2552] * np.conj(c[0:504]))
+        assert abs(fc[i] - fc_ref) <= 1e-3 * abs(fc_ref) + 1e-3, (phase, i, fc[i], fc_ref)
+    iq.free()
+    print("worst |q_gpu - q_oracle|", phase, worst)
+    assert worst <= SOFT_TOL, (phase, worst)
+
+
 # ---------------------------------------------------------------- pipeline
 def _pipeline_decode(ctx, ens_list, F, subch, cfo=0.0, snr=300.0, runs=2):
     import dabamd

@@ -303,3 +303,39 @@ def test_scan_mode_counts_attempts_like_reference(ctx):
     finally:
         pipe.close()
         diq.free()
+
+
+def test_pipeline_iq_display_matches_reference_feed(ctx):
+    """the constellation feed (ofdmDecoder::processToken, ofdm-decoder.cpp:192-206): the
+    pipeline's symbol-2 display carriers of every 8th frame equal the oracle's iqBuffer
+    pushes (fft_buffer[0, K/2) and [T_u-1-K/2, T_u-1) of the same frame) within 1e-5 of
+    the spectrum's RMS, under a carrier offset (the NCO-mixed samples' FFT)"""
+    import dabamd
+    from dabamd.synth import Ensemble
+    F, runs = 8, 2
+    sub = [(0, 96, 128, 3, 1)]
+    e = Ensemble(F * runs + 1, subch=[s + (0,) for s in sub], snr_db=20.0, cfo_hz=1300.0)
+    iq = e.generate(55, truth=False)["iq"]
+    n, info, _, disp, dfr, _ = orc.ofdm_run_display(iq, F * runs)
+    assert n == F * runs and list(dfr) == [7, 15]
+    diq = ctx.put(iq[None, :])
+    subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, 0) for s in sub]
+    pipe = dabamd.Pipeline(ctx, 1, F, subs)
+    pipe.set_display(True)
+    got = {}
+    try:
+        for r in range(runs):
+            pipe.run(diq, e.length, [e.length])
+            frames, si = pipe.frames()
+            for f in range(F):
+                assert frames[f].window == info[r * F + f].window_start
+                got[r * F + f] = pipe.iq_display(0, f)
+    finally:
+        pipe.close()
+        diq.free()
+    for k, fidx in enumerate(dfr):
+        want = disp[k]
+        rms = np.sqrt(np.mean(np.abs(want) ** 2))
+        err = np.abs(got[int(fidx)] - want).max() / rms
+        print("frame", fidx, "max |gpu - oracle| / rms", err)
+        assert err <= 1e-5, (fidx, err)
