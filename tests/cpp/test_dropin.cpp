@@ -330,7 +330,14 @@ int main() {
         {
             dabgpu::DabParams p;
             dabgpu::setModeParameters(&p, 1);
-            dabgpu::ofdmDecoder od(&p, 1);
+            // the reference's argument list (ofdm-decoder.h:40-44): iqBuffer, refTable, the GUI
+            dabgpu::RingBuffer<dabgpu::DSPCOMPLEX> iqBuffer(2 * 1536);
+            std::vector<dabgpu::DSPCOMPLEX> refTable(2048);
+            int showIQ = 0;
+            dabgpu::ofdmDecoder::signals dsig;
+            dsig.showIQ = [&](int amount) { showIQ = amount; };
+            dabgpu::ofdmDecoder od(&p, &iqBuffer, refTable.data(), dsig, 1);
+            dabgpu::ofdmDecoder::iq_count = 7;       // this frame's symbol 2 is the 8th display token
             const orc_frame_info &fi = info[1];
             const int64_t b0 = fi.window_start + fi.start_index;
             auto mixed = [&](int64_t first, int64_t count, int32_t lp0, int32_t phase, int64_t origin) {
@@ -362,12 +369,35 @@ int main() {
                 int16_t gi[3072], oi[3072];
                 od.processToken((dabgpu::DSPCOMPLEX *)sym.data(), gi, l);
                 orc_process_token(sym.data(), pref, oi, nullptr);
+                if (l == 2) {                         // ofdm-decoder.cpp:192-206: the carriers pushed
+                    float X[4096];
+                    orc_fft2048(sym.data() + 2 * 504, X, 0);
+                    std::vector<dabgpu::DSPCOMPLEX> got(1536);
+                    const int n = iqBuffer.getDataFromBuffer(got.data(), 1536);
+                    double rms = 0, err = 0;
+                    for (int i = 0; i < 1536; i++) {
+                        const int b = i < 768 ? i : 2047 - 768 + (i - 768);
+                        const dabgpu::DSPCOMPLEX w(X[2 * b], X[2 * b + 1]);
+                        rms += std::norm(w);
+                        err = std::max(err, (double)std::abs(got[i] - w));
+                    }
+                    rms = std::sqrt(rms / 1536);
+                    CHECK(n == 1536 && showIQ == 1536 && err <= 1e-5 * rms,
+                          "iqBuffer: %d values, showIQ(%d), max error %g of rms %g", n, showIQ, err, rms);
+                }
                 for (int i = 0; i < 3072; i++) {
                     bad += gi[i] != oi[i];
                     big += std::abs(gi[i] - oi[i]) > 1;
                 }
             }
             CHECK(big == 0 && bad <= 30, "ofdmDecoder::processToken: %ld soft bits differ (%ld by more than 1)", bad, big);
+            CHECK(iqBuffer.GetRingBufferReadAvailable() == 0, "one display token only");
+            {                                         // get_snr (ofdm-decoder.cpp:212-230) of block 0's spectrum
+                float X[4096];
+                orc_fft2048(blk0.data(), X, 0);
+                const int16_t os = orc_get_snr(X), gs = od.get_snr((dabgpu::DSPCOMPLEX *)X);
+                CHECK(std::abs(os - gs) <= 1, "get_snr %d vs %d", gs, os);
+            }
             std::printf("ofdmDecoder: ok (%ld of %d soft bits at a rounding boundary)\n", bad, 75 * 3072);
         }
         // ofdmProcessor pulling from a virtualInput, feeding ficHandler and mscHandler

@@ -55,3 +55,22 @@ def test_raw_drops_odd_byte(tmp_path):
     b.tofile(p)
     got = dabamd.read_raw(p)
     assert got.size == 10 and np.array_equal(np.asarray(got), b[:10])
+
+
+def test_ringbuffer_and_sdr_dump_standin(tmp_path):
+    """the drop-in RingBuffer (ringbuffer.h:127-319 contract, SPSC stress under TSan) and
+    the libsndfile stand-in behind ofdmProcessor::startDumping(SNDFILE *): the .sdr it
+    writes is what gui.cpp:879-883 asks sf_open for (WAV, PCM16, 2 channels, 2.048 MHz)"""
+    import subprocess
+    import wave
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    subprocess.run(["make", "-s", "-f", os.path.join(root, "tests", "cpp", "Makefile")], check=True)
+    out = tmp_path / "dump.sdr"
+    r = subprocess.run([os.path.join(root, "tests", "cpp", "build", "test_ringbuffer"), str(out)],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "RINGBUFFER OK" in r.stdout, r.stdout + r.stderr
+    with wave.open(str(out)) as w:
+        assert (w.getnchannels(), w.getsampwidth(), w.getframerate(), w.getnframes()) == (2, 2, 2048000, 3 * 4096)
+        d = np.frombuffer(w.readframes(3 * 4096), "<i2").reshape(-1, 2)
+    k = np.arange(3 * 4096)
+    assert np.array_equal(d[:, 0], (k - 6000).astype(np.int16)) and np.array_equal(d[:, 1], (-k).astype(np.int16))
