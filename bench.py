@@ -44,6 +44,7 @@ sys.path.insert(0, os.path.join(ROOT, "sdr-j-dab_amd"))
 TF, TNULL, TU, TS = 196608, 2656, 2048, 2552
 RT_SYMBOLS = 76 / 0.096            # symbols/s of one real-time Mode-I ensemble (791.67)
 HBM_PEAK_GBS = 8000.0              # MI355X_MICROARCH.md chip table (spec)
+SYMBOL_BYTES = 8 * TS + 2 * 3072   # algorithmic bytes per OFDM symbol (26,560)
 VALU_PEAK_TOPS = 256 * 4 * 32 * 2.4e9 / 1e12   # int32 lane-ops/s: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz
 C3_SUBCH = [(96 * i, 96, 128, 3, 1, 0) for i in range(9)]   # (startAddr, CUs, kbps, level, uep, dab+)
 # C5: 16 ensembles x 16 DAB+ subchannels (64 kbit/s EEP-3A, 48 CUs, RSDims 8) = 256
@@ -426,6 +427,14 @@ def main():
     ap.add_argument("--solo-steps", type=int, default=2,
                     help="steps after the timed region with every kernel alone on the device (profiling mode 3): "
                          "per-kernel times without overlap, to name the dominant kernel")
+    ap.add_argument("--delivered-steps", type=int, default=10,
+                    help="timed steps after the main measurement whose FIC bits + CRCs and MSC bytes (8 bits per "
+                         "byte) are copied to pinned host memory while the next step decodes (dabgpu_pipe_fetch): "
+                         "the delivered rate, reported beside value")
+    ap.add_argument("--sync-loss-steps", type=int, default=8,
+                    help="timed steps (per acquisition mode) in which one stream every 2 steps loses sync (an "
+                         "interferer over 1.5 frames: findIndex fails, goto notSynced) -- the price of a sync loss, "
+                         "with the null search inside the run and in the background (DABGPU_CTL_ACQ_ASYNC)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -444,7 +453,10 @@ def main():
     dabplus = any(s[5] for s in SUBCH)
     E, F = args.ensembles or E_default, args.frames
     # +1 step: the checked pass; then the solo steps
-    total_frames = F * (args.warmup + args.steps + 1 + args.solo_steps) + 1
+    deliv_steps = args.delivered_steps + 1 if args.delivered_steps > 0 else 0     # + one untimed warm-up
+    loss_steps = 2 * (args.sync_loss_steps + 1) if args.sync_loss_steps > 0 else 0  # two modes, + one each
+    # (+ 2F: a stream that loses sync skips frames and reaches the end of its samples sooner)
+    total_frames = F * (args.warmup + args.steps + 1 + args.solo_steps + deliv_steps + loss_steps + (2 if loss_steps else 0)) + 1
     ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0, cfo_hz=args.cfo)
     P = period_frames(F, dabplus)
     ctx = dabamd.Context(rank_device(local))
@@ -566,6 +578,18 @@ def main():
         pipe.sync()
         tm_alone = {k: v[0] / max(v[1], 1) for k, v in pipe.timing().items()}
         pipe.set_profiling(False)
+    # the delivered leg: every step's results leave the GPU (FIC bits + CRC flags, the MSC
+    # packed 8 bits per byte, DAB+ superframe records + bytes) into pinned host memory,
+    # each copy queued behind its run's channel decoding while the next run decodes
+    delivered = None
+    if deliv_steps and not rccl:
+        k0 = ck + 1 + args.solo_steps
+        delivered = delivered_leg(dabamd, ctx, pipe, step, k0, deliv_steps - 1, E, F, SUBCH, dabplus, dist, truth, P)
+    sync_loss = None
+    if loss_steps and not rccl and E >= 2:
+        k0 = ck + 1 + args.solo_steps + deliv_steps
+        sync_loss = sync_loss_leg(dabamd, ctx, pipe, step, k0, args.sync_loss_steps, E, F, stride, diq, dist,
+                                  el / args.steps * 1e3)
     sf_ok = None
     if dp is not None:
         info = dp[0]
@@ -642,7 +666,15 @@ def main():
         "dabplus_last_step": sf_ok,
         "gen_seconds": gen_s,
         "acquire_ms": {"streams": E, "ms": acquire_ms, "note": "initial null search of every stream (host-timed, first launch)"},
+        # the whole step priced at the front end's algorithmic bytes
+        "hbm_frac_step": value / world * SYMBOL_BYTES / (HBM_PEAK_GBS * 1e9),
+        "hbm_frac_step_note": "symbols/s per GPU x 26,560 B (8 T_s cf32 in + 2 x 3072 int16 out per symbol) / 8 TB/s",
     }
+    if delivered is not None:
+        out["delivered_symbols_per_s"] = delivered.pop("value")
+        out["delivered"] = delivered
+    if sync_loss is not None:
+        out["sync_loss"] = sync_loss
     if probe is not None:
         out["stream_split"] = probe
     if rccl:
@@ -668,6 +700,123 @@ def main():
             "realtime_ensembles": cpu["value"] / RT_SYMBOLS,
         }
     print(json.dumps(out))
+
+
+def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist, truth, P):
+    """`steps` timed steps whose outputs are copied to pinned host memory (two sets,
+    alternating like the pipeline's device outputs), each copy on its run's back-end
+    stream behind the channel decoding (dabgpu_pipe_fetch), overlapping the next run.
+    The last step's host copy of ensemble 0 is checked against the transmitted bits."""
+    pipe.sync()
+    pipe.set_packed(True)
+    ns = len(subch)
+    n_fic, n_crc = E * F * 4 * 768, E * F * 12
+    n_msc = E * 4 * F * ns * pipe.msc_stride_packed
+    nd = len(pipe.dp)
+    n_sfi = E * 4 * F * nd * 16 if nd else 0                     # dabgpu_superframe records
+    n_sf = E * 4 * F * nd * pipe.sf_stride if nd else 0
+    total = n_fic + n_crc + n_msc + n_sfi + n_sf
+    hb = [dabamd.HostBuf(ctx, total) for _ in range(2)]
+    valids = [None, None]
+
+    def one(k, i):
+        valid, _ = step(k)
+        h = hb[i & 1]
+        o = 0
+        for src, n in ((pipe.fic_d, n_fic), (pipe.crc_d, n_crc), (pipe.msc_d, n_msc)) + \
+                (((pipe.sfi_d, n_sfi), (pipe.sf_d, n_sf)) if nd else ()):
+            if n:
+                pipe.fetch(h, src, n, o)
+            o += n
+        valids[i & 1] = valid
+
+    one(k0, 0)                                                  # untimed: the packed format's first run
+    pipe.sync()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for i in range(steps - 1):
+        one(k0 + 1 + i, i + 1)
+    st0 = pipe.state(0)
+    one(k0 + steps, steps)
+    pipe.sync()
+    el = allreduce_max(dist, time.perf_counter() - t0)
+    barrier(dist)
+    st1 = pipe.state(0)
+    h = hb[steps & 1]
+    fic = h.view(np.uint8, (E, F, 4, 768))
+    crc = h.view(np.uint8, (E, F, 12), n_fic)
+    msc = np.unpackbits(h.view(np.uint8, (E, 4 * F, ns, pipe.msc_stride_packed), n_fic + n_crc), axis=-1)
+    check = check_step(truth, P, st0, st1, fic, crc, msc, valids[steps & 1], subch)
+    pipe.set_packed(False)
+    for b in hb:
+        b.free()
+    world = dist.get_world_size() if dist is not None else 1
+    return {"value": world * E * F * 76 * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
+            "bytes_to_host_per_step": total, "pcie_GBps": total * steps / el / 1e9,
+            "msc_format": "8 bits per byte, msb first (dabgpu_pipe_set_packed)",
+            "checked_last_step_from_host_memory": check,
+            "note": "FIC bits + CRC flags + packed MSC bytes" + (" + DAB+ superframe records and bytes" if nd else "")
+                    + " of every step copied to pinned host memory behind its run's channel decoding "
+                      "(dabgpu_pipe_fetch), overlapping the next run"}
+
+
+def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, base_ms):
+    """The price of a sync loss (ofdm-processor.cpp:354-357: findIndex fails -> notSynced,
+    the null search from where the stream is).  Before step k0 + 2j + 1 of each mode, stream
+    j gets an interferer over 300,000 samples (1.5 frames) in the middle of that step's
+    frames: a carrier at +100 kHz whose PRS correlation is flat.  Mode "sync": the run waits
+    for the stream's null search (k_acquire, one wave) and still delivers F frames of every
+    stream; mode "async" (DABGPU_CTL_ACQ_ASYNC): the search runs in the background and the
+    run goes on without that stream.  Reported: ms per step against the loss-free steps
+    (base_ms), the hit per loss, and the frames decoded."""
+    n = 300000
+    rng = np.random.default_rng(11)
+    ph = 2 * np.pi * 100e3 / 2048000 * np.arange(n)
+    jam = np.empty((n, 2), np.float32)
+    jam[:, 0] = np.cos(ph) + rng.normal(0, 0.1, n)
+    jam[:, 1] = np.sin(ph) + rng.normal(0, 0.1, n)
+    res = {}
+    j = 0
+    for mode in ("sync", "async"):
+        pipe.sync()
+        pipe.control(dabamd.CTL_ACQ_ASYNC if mode == "async" else dabamd.CTL_ACQ_SYNC)
+        step(k0)                                           # untimed
+        k0 += 1
+        frames0 = [pipe.state(s).cif_count // 4 for s in range(E)]
+        pos0 = [pipe.state(s).next_pos for s in range(E)]
+        losses = 0
+        for i in range(0, steps, 2):
+            # stream j: the interferer half-way through the frames of step k0 + i + 1
+            s = j % E
+            at = pos0[s] + (i + 1) * F * TF + F // 2 * TF + 40000
+            if at + n < stride:
+                diq.upload_at(jam.reshape(-1), (s * 2 * stride + 2 * at) * 4)
+                losses += 1
+            j += 1
+        pipe.sync()
+        barrier(dist)
+        t0 = time.perf_counter()
+        for i in range(steps):
+            step(k0 + i)
+        pipe.sync()
+        el = allreduce_max(dist, time.perf_counter() - t0)
+        barrier(dist)
+        k0 += steps
+        st = [pipe.state(s) for s in range(E)]
+        frames = sum(st[s].cif_count // 4 - frames0[s] for s in range(E))
+        ms = el / steps * 1e3
+        res[mode] = {"steps": steps, "losses": losses, "ms_per_step": ms,
+                     "hit_ms_per_loss": (ms - base_ms) * steps / max(losses, 1),
+                     "hit_steps_per_loss": (ms - base_ms) * steps / max(losses, 1) / base_ms,
+                     "frames_decoded": int(frames), "frames_loss_free": E * F * steps,
+                     "resyncs": int(sum(x.resyncs for x in st)), "acquiring_at_end": int(sum(x.acquiring for x in st))}
+    pipe.sync()
+    pipe.control(dabamd.CTL_ACQ_SYNC)
+    res["base_ms_per_step"] = base_ms
+    res["note"] = ("one stream every 2 steps loses sync (interferer over 1.5 frames, findIndex fails); sync: the run "
+                   "waits for its null search (k_acquire); async: the search runs in the background and that stream "
+                   "rejoins a later run (its frames delivered later, frame for frame the same)")
+    return res
 
 
 def _crc_flip():

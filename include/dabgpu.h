@@ -135,6 +135,9 @@ int         dabgpu_free(dabgpu_ctx *ctx, void *dptr);
 int         dabgpu_memcpy_h2d(dabgpu_ctx *ctx, void *dst_d, const void *src_h, size_t bytes);
 int         dabgpu_memcpy_d2h(dabgpu_ctx *ctx, void *dst_h, const void *src_d, size_t bytes);
 int         dabgpu_memset_d(dabgpu_ctx *ctx, void *dst_d, int value, size_t bytes);
+/* page-locked host memory (DMA without the pageable bounce: dabgpu_pipe_fetch targets) */
+int         dabgpu_host_alloc(dabgpu_ctx *ctx, size_t bytes, void **h);
+int         dabgpu_host_free(dabgpu_ctx *ctx, void *h);
 /* device-to-device copy on the context stream (asynchronous; regions must not overlap) */
 int         dabgpu_memcpy_d2d(dabgpu_ctx *ctx, void *dst_d, const void *src_d, size_t bytes);
 /* HIP events on the context stream, for timing (ms between two marks) */
@@ -273,7 +276,7 @@ typedef struct {
     int32_t attempts;          /* the reference's `attempts` counter (ofdm-processor.cpp:274-314) */
     int32_t no_signal;         /* No_Signal_Found emissions (scan mode, > 5 failed attempts) */
     int32_t frames_run;        /* frames this stream committed in the last dabgpu_pipe_run */
-    int32_t reserved;
+    int32_t acquiring;         /* 1: a background null search (DABGPU_CTL_ACQ_ASYNC) is running */
 } dabgpu_stream_state;
 
 /* Per-frame record of the last run (the observables ofdmProcessor / ofdmDecoder
@@ -331,13 +334,31 @@ int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info_h);
  *   DABGPU_CTL_COARSE_OFF   coarseCorrectorOff() (:503-505)
  *   DABGPU_CTL_SCAN_ON/OFF  set_scanMode(bool) (:507-509): count No_Signal_Found
  *   DABGPU_CTL_RESYNC       drop sync: the next run searches the null symbol again from
- *                           the stream's current position (goto notSynced) */
+ *                           the stream's current position (goto notSynced)
+ *   DABGPU_CTL_ACQ_ASYNC    (stream ignored) a stream that needs the null search -- a sync
+ *                           loss, ofdm-processor.cpp:354-357 -- gets it in the background on
+ *                           a low-priority stream while the run goes on without it; the first
+ *                           run after the search finished continues that stream from where it
+ *                           found the null (its frames are the same, delivered later: it
+ *                           decodes fewer than n_frames in the runs it misses, with
+ *                           DABGPU_OK).  iq_d must stay valid until the search ends
+ *                           (dabgpu_stream_state.acquiring).  dabgpu_pipe_sync does not wait
+ *                           for a background search.
+ *   DABGPU_CTL_ACQ_SYNC     (default) the run waits for the search and delivers n_frames
+ *   DABGPU_CTL_INJECT_BOUNDS fault injection (stream ignored): the next run's MSC decoder
+ *                           is handed a subchannel offset past the soft-bit ring; its
+ *                           kernels refuse it (zeros read instead), and dabgpu_pipe_sync or
+ *                           the next run reports DABGPU_E_BOUNDS once -- the error path of
+ *                           the back-end streams, for tests */
 #define DABGPU_CTL_RESET      1
 #define DABGPU_CTL_COARSE_ON  2
 #define DABGPU_CTL_COARSE_OFF 3
 #define DABGPU_CTL_SCAN_ON    4
 #define DABGPU_CTL_SCAN_OFF   5
 #define DABGPU_CTL_RESYNC     6
+#define DABGPU_CTL_ACQ_ASYNC  7
+#define DABGPU_CTL_ACQ_SYNC   8
+#define DABGPU_CTL_INJECT_BOUNDS 9
 int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op);
 /* Wait until everything the pipeline enqueued is done.  The FIC/MSC/DAB+ outputs
  * of run r are written by back-end stream r & 1 (overlapping run r+1's OFDM front
@@ -378,6 +399,17 @@ int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *frames_h, int32_t *start_in
  * Which frames the GUI is shown (every 8th) is the caller's choice, as in the
  * reference.  Costs 12 KB of HBM writes per frame while on. */
 int dabgpu_pipe_set_display(dabgpu_pipe *p, int on);
+/* MSC output format of the following runs: on = 0 (default) one bit per byte, as
+ * deconvolve delivers it (viterbi.cpp:240-241); on = 1 eight bits per byte, msb first
+ * (the packing of mp4Processor::addtoFrame, mp4processor.cpp:115-121 -- numpy packbits
+ * order): msc_stride is then in bytes (>= 3 * bitRate).  The DAB+ layer reads either. */
+int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on);
+/* Copy bytes from an output buffer of the last dabgpu_pipe_run (or dabgpu_pipe_dabplus)
+ * to host memory, asynchronously, behind that run's channel decoding on its back-end
+ * stream: the results reach the host while the next run decodes.  Complete after
+ * dabgpu_pipe_sync, or once the run after next has started (it waits for this back
+ * end).  dst_h should be dabgpu_host_alloc memory (else the copy may synchronise). */
+int dabgpu_pipe_fetch(dabgpu_pipe *p, void *dst_h, const void *src_d, size_t bytes);
 int dabgpu_pipe_iq_display(dabgpu_pipe *p, int stream, int frame, float *carriers_h);
 
 #ifdef __cplusplus

@@ -120,6 +120,7 @@ struct VitJob {
     uint8_t *out;
     int64_t out_stride;             // bytes per codeword
     int32_t prbs;                   // xor energy-dispersal sequence
+    int32_t packed;                 // out: 8 bits per byte, msb first (else one bit per byte)
     const uint32_t *prbs_words;     // PRBS packed 32 bits per word, bit i = prbs[32w+i]
     const uint8_t *valid;           // optional per-codeword flag: 0 = skip
     // SRC_MSC / SRC_FIC: inverse depuncturing tables, Profile::frag uint16 mother-code
@@ -137,6 +138,7 @@ struct DpState {
 struct DpJob {
     const uint8_t *msc;             // MSC bits of the run: [S][ncif][nsub][msc_stride]
     int32_t msc_stride, ncif, nsub, ndp, nstreams;
+    int32_t packed;                 // msc holds bytes (8 bits msb first), else one bit per byte
     const int64_t *cif0s;           // [stream] CIF index of the run's first CIF slot
     const int32_t *ncifs;           // [stream] CIFs the stream delivered in the run
     const int32_t *dp_sub;          // [ndp] subchannel index of each DAB+ subchannel

@@ -486,6 +486,19 @@ int dabgpu_memcpy_d2h(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
     HIPCHK(hipStreamSynchronize(c->stream));
     return 0;
 }
+int dabgpu_host_alloc(dabgpu_ctx *c, size_t bytes, void **h) {
+    if (!c || !h) return fail(DABGPU_E_ARG, "bad args");
+    *h = nullptr;
+    if (!bytes) return 0;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipHostMalloc(h, bytes, hipHostMallocDefault));
+    return 0;
+}
+int dabgpu_host_free(dabgpu_ctx *c, void *h) {
+    if (!c) return fail(DABGPU_E_ARG, "bad args");
+    if (h) HIPCHK(hipHostFree(h));
+    return 0;
+}
 int dabgpu_memcpy_d2d(dabgpu_ctx *c, void *dst, const void *src, size_t bytes) {
     if (!c) return fail(DABGPU_E_ARG, "null ctx");
     HIPCHK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, c->stream));
@@ -843,6 +856,24 @@ struct dabgpu_pipe {
     // the iqBuffer feed (dabgpu_pipe_set_display): symbol 2's display carriers per ring slot
     float2 *disp_d = nullptr;        // [S][R][K]
     bool display = false;
+    bool packed = false;             // MSC output 8 bits per byte (dabgpu_pipe_set_packed)
+    // background null search (DABGPU_CTL_ACQ_ASYNC): a stream that loses sync is searched
+    // on its own low-priority stream while the others keep decoding; its results are
+    // taken by the first dabgpu_pipe_run after they arrive
+    bool acq_async = false;
+    hipStream_t as = nullptr;
+    hipEvent_t ev_acq = nullptr;
+    AcqJob *acq_jobs_d = nullptr;
+    AcqResult *acq_res_d = nullptr, *h_acq = nullptr;   // [S]
+    AcqJob *h_acq_jobs = nullptr;                         // [S] pinned staging
+    std::vector<int> acq_who;
+    std::vector<char> acquiring;                          // [S]
+    bool acq_inflight = false;
+    // fault injection (DABGPU_CTL_INJECT_BOUNDS): the next run's MSC job gets a subchannel
+    // table whose first entry points past the ring, which the Viterbi loader refuses
+    bool inject_bounds = false;
+    int32_t *substart_bad_d = nullptr;
+    bool last_msc_packed = false;
     // optional per-stage kernel timing (HIP events on the stage's stream)
     int profiling = 0;                          // 1: last run, 2: every run since enabled, 3: 2 + stages alone
     std::vector<hipEvent_t> ev_pool;
@@ -881,7 +912,11 @@ static hipError_t prof_mark(dabgpu_pipe *p, int stage, bool start) {
 static int back_errors(dabgpu_pipe *p, bool wait) {
     for (int par = 0; par < 2; par++) {
         if (!p->back_rec[par]) continue;
-        if (!wait && hipEventQuery(p->ev_back[par]) != hipSuccess) continue;
+        if (!wait) {
+            const hipError_t q = hipEventQuery(p->ev_back[par]);
+            if (q == hipErrorNotReady) continue;
+            if (q != hipSuccess) return fail(DABGPU_E_HIP, "back-end stream %d: %s", par, hipGetErrorString(q));
+        }
         const int32_t e = *(volatile int32_t *)&p->h_berr[par];
         if (e) {
             p->h_berr[par] = 0;
@@ -1053,6 +1088,15 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1], p->ev_dp, p->ev_copy[0], p->ev_copy[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
+    if (p->as) {                                    // a background null search still running
+        (void)hipStreamSynchronize(p->as);
+        (void)hipStreamDestroy(p->as);
+    }
+    if (p->ev_acq) (void)hipEventDestroy(p->ev_acq);
+    for (void *h : {(void *)p->h_acq, (void *)p->h_acq_jobs})
+        if (h) (void)hipHostFree(h);
+    for (void *x : {(void *)p->acq_jobs_d, (void *)p->acq_res_d})
+        if (x) (void)hipFree(x);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
     for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_cif0,
                     (void *)p->h_ncif, (void *)p->h_slots, (void *)p->h_berr})
@@ -1061,13 +1105,39 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->cif0_d, (void *)p->ncif_d, (void *)p->berr_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d,
-                    (void *)p->dp_cand_d, (void *)p->disp_d})
+                    (void *)p->dp_cand_d, (void *)p->disp_d, (void *)p->substart_bad_d})
         if (x) (void)hipFree(x);
     delete p;
     return 0;
 }
 
 }  // extern "C"
+
+static AcqJob acq_job(const dabgpu_pipe *p, const StreamSt &x, int s, int64_t stride, const int64_t *n_avail) {
+    AcqJob j;
+    memset(&j, 0, sizeof j);
+    j.iq_base = stride * s;
+    j.start = x.window;
+    j.end = n_avail[s];
+    j.local_phase = x.lp;
+    j.phase = x.coarse + x.fine;
+    // the kernel enters notSynced (attempts++) first; a cut attempt is repeated whole
+    j.attempts = x.attempts - (x.in_attempt ? 1 : 0);
+    j.scan = p->scan ? 1 : 0;
+    return j;
+}
+// a search's outcome into the stream state; 1 if it found the end of a null symbol
+static int acq_apply(StreamSt &x, const AcqResult &r) {
+    x.lp = r.local_phase;
+    x.window = r.window;
+    x.attempts = r.attempts;
+    x.in_attempt = r.status != 0;
+    x.no_signal += r.no_signal;
+    if (r.status != 0) return 0;
+    x.synced = true;
+    x.acquisitions++;
+    return 1;
+}
 
 // Null-symbol search (notSynced .. SyncOnEndNull, ofdm-processor.cpp:274-338) for the
 // streams `who` of `cur`, each from its current position (window, localPhase) with
@@ -1080,19 +1150,7 @@ static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     found = 0;
     if (who.empty()) return 0;
     std::vector<AcqJob> jobs;
-    for (int s : who) {
-        AcqJob j;
-        memset(&j, 0, sizeof j);
-        j.iq_base = stride * s;
-        j.start = cur[s].window;
-        j.end = n_avail[s];
-        j.local_phase = cur[s].lp;
-        j.phase = cur[s].coarse + cur[s].fine;
-        // the kernel enters notSynced (attempts++) first; a cut attempt is repeated whole
-        j.attempts = cur[s].attempts - (cur[s].in_attempt ? 1 : 0);
-        j.scan = p->scan ? 1 : 0;
-        jobs.push_back(j);
-    }
+    for (int s : who) jobs.push_back(acq_job(p, cur[s], s, stride, n_avail));
     void *jd = nullptr, *rd = nullptr;
     int rc = scratch(c, SC_MISC, sizeof(AcqJob) * jobs.size(), &jd);
     if (rc) return rc;
@@ -1102,19 +1160,37 @@ static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     std::vector<AcqResult> res(jobs.size());
     HIPCHK(hipMemcpyAsync(res.data(), rd, sizeof(AcqResult) * jobs.size(), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
-    for (size_t i = 0; i < jobs.size(); i++) {
-        StreamSt &S = cur[who[i]];
-        S.lp = res[i].local_phase;
-        S.window = res[i].window;
-        S.attempts = res[i].attempts;
-        S.in_attempt = res[i].status != 0;
-        S.no_signal += res[i].no_signal;
-        if (res[i].status == 0) {
-            S.synced = true;
-            S.acquisitions++;
-            found++;
-        }
+    for (size_t i = 0; i < jobs.size(); i++) found += acq_apply(cur[who[i]], res[i]);
+    return 0;
+}
+
+// Background form (DABGPU_CTL_ACQ_ASYNC): the same search launched on the pipeline's
+// acquisition stream without waiting; acq_collect applies the results once they are in.
+static int acquire_streams_async(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
+                                 const std::vector<int> &who, const std::vector<StreamSt> &cur) {
+    for (size_t i = 0; i < who.size(); i++) p->h_acq_jobs[i] = acq_job(p, cur[who[i]], who[i], stride, n_avail);
+    const size_t n = who.size();
+    HIPCHK(hipMemcpyAsync(p->acq_jobs_d, p->h_acq_jobs, sizeof(AcqJob) * n, hipMemcpyHostToDevice, p->as));
+    HIPCHK(launch_acquire(p->as, iq, p->acq_jobs_d, (int)n, p->c->osc, p->acq_res_d));
+    HIPCHK(hipMemcpyAsync(p->h_acq, p->acq_res_d, sizeof(AcqResult) * n, hipMemcpyDeviceToHost, p->as));
+    HIPCHK(hipEventRecord(p->ev_acq, p->as));
+    p->acq_who = who;
+    for (int s : who) p->acquiring[s] = 1;
+    p->acq_inflight = true;
+    return 0;
+}
+static int acq_collect(dabgpu_pipe *p, bool wait) {
+    if (!p->acq_inflight) return 0;
+    const hipError_t q = wait ? hipEventSynchronize(p->ev_acq) : hipEventQuery(p->ev_acq);
+    if (q == hipErrorNotReady) return 0;
+    if (q != hipSuccess) return fail(DABGPU_E_HIP, "background null search: %s", hipGetErrorString(q));
+    for (size_t i = 0; i < p->acq_who.size(); i++) {
+        const int s = p->acq_who[i];
+        (void)acq_apply(p->st[s], p->h_acq[i]);
+        p->acquiring[s] = 0;
     }
+    p->acq_who.clear();
+    p->acq_inflight = false;
     return 0;
 }
 
@@ -1418,8 +1494,10 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     dabgpu_ctx *c = p->c;
     const int S = p->S, F = p->F;
     const bool do_msc = msc_bits && p->NSUB > 0;
-    if (do_msc && msc_stride < p->max_nbits) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, p->max_nbits);
+    const int need = p->packed ? (p->max_nbits + 7) / 8 : p->max_nbits;
+    if (do_msc && msc_stride < need) return fail(DABGPU_E_ARG, "msc_stride %d < %d", msc_stride, need);
     if (int rc = back_errors(p, false)) return rc;
+    if (int rc = acq_collect(p, false)) return rc;        // a background null search that finished
     p->last_frames.assign((size_t)S * F, dabgpu_frame());
     p->last_si.assign((size_t)S * F, 0);
     p->last_info.assign((size_t)S * F, dabgpu_frame_info());
@@ -1492,9 +1570,10 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             JM.ring = p->R;
             JM.cif0s = p->cif0_d + (size_t)par * S;
             JM.ncifs = p->ncif_d + (size_t)par * S;
-            JM.sub_start = p->substart_d;
+            JM.sub_start = p->inject_bounds ? p->substart_bad_d : p->substart_d;
             JM.out = msc_bits;
             JM.out_stride = msc_stride;
+            JM.packed = p->packed ? 1 : 0;
             JM.prbs = 1;
             JM.prbs_words = c->prbs;
             JM.dec = p->dec_d[par];
@@ -1575,9 +1654,15 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     for (int it = 0; it < 64 * F + 64; it++) {
         std::vector<int> who;
         for (int s = 0; s < S; s++)
-            if (!cur[s].synced && done[s] < F) who.push_back(s);
+            if (!cur[s].synced && done[s] < F && !(p->acq_async && p->acquiring[s])) who.push_back(s);
         int found = 0;
-        if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) return bail(rc);
+        if (p->acq_async) {
+            // in the background: this run goes on without those streams (one batch in flight)
+            if (!who.empty() && !p->acq_inflight)
+                if (int rc = acquire_streams_async(p, iq, stride, n_avail, who, cur)) return bail(rc);
+        } else if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) {
+            return bail(rc);
+        }
         bool progress = false, lost = false;
         std::function<int()> after;
         if (spec && it == 0 && found == 0)
@@ -1595,7 +1680,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     }
     bool all = true;
     for (int s = 0; s < S; s++) {
-        if (done[s] != F) all = false;
+        if (done[s] != F && !(p->acq_async && (p->acquiring[s] || !cur[s].synced))) all = false;
         cur[s].frames_run = done[s];
     }
     std::vector<int32_t> slot((size_t)S * F, -1);
@@ -1613,8 +1698,10 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     HIPCHK(hipEventRecord(p->ev_back[par], bs));
     p->back_rec[par] = true;
     p->run_idx++;
+    p->inject_bounds = false;
     p->last_msc = do_msc ? msc_bits : nullptr;
     p->last_msc_stride = msc_stride;
+    p->last_msc_packed = p->packed;
     if (msc_valid)
         for (int s = 0; s < S; s++)
             for (int q = 0; q < 4 * F; q++)
@@ -1672,6 +1759,7 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     memset(&J, 0, sizeof J);
     J.msc = p->last_msc;
     J.msc_stride = p->last_msc_stride;
+    J.packed = p->last_msc_packed ? 1 : 0;
     J.ncif = 4 * p->F;
     J.nsub = p->NSUB;
     J.ndp = p->NDP;
@@ -1722,7 +1810,7 @@ int dabgpu_pipe_state(dabgpu_pipe *p, int s, dabgpu_stream_state *o) {
     o->attempts = x.attempts;
     o->no_signal = x.no_signal;
     o->frames_run = x.frames_run;
-    o->reserved = 0;
+    o->acquiring = (p->acq_async && !p->acquiring.empty() && p->acquiring[s]) ? 1 : 0;
     return 0;
 }
 
@@ -1737,6 +1825,38 @@ int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op) {
     if (!p || stream < -1 || stream >= p->S) return fail(DABGPU_E_ARG, "bad args");
     if (op == DABGPU_CTL_SCAN_ON || op == DABGPU_CTL_SCAN_OFF) {      // set_scanMode (one flag, like the reference's)
         p->scan = op == DABGPU_CTL_SCAN_ON;
+        return 0;
+    }
+    if (op == DABGPU_CTL_INJECT_BOUNDS) {
+        if (p->NSUB == 0) return fail(DABGPU_E_STATE, "no MSC subchannel to corrupt");
+        if (!p->substart_bad_d) {
+            HIPCHK(hipMalloc((void **)&p->substart_bad_d, sizeof(int32_t) * p->NSUB));
+            std::vector<int32_t> bad(p->NSUB);
+            for (int i = 0; i < p->NSUB; i++) bad[i] = p->sub[i].startAddr * 64;
+            bad[0] = 0x40000000;                        // far past any ring (no int32 overflow in the loader)
+            HIPCHK(hipMemcpy(p->substart_bad_d, bad.data(), sizeof(int32_t) * p->NSUB, hipMemcpyHostToDevice));
+        }
+        p->inject_bounds = true;
+        return 0;
+    }
+    if (op == DABGPU_CTL_ACQ_ASYNC || op == DABGPU_CTL_ACQ_SYNC) {
+        if (op == DABGPU_CTL_ACQ_SYNC) {
+            if (int rc = acq_collect(p, true)) return rc;   // a search in flight completes first
+            p->acq_async = false;
+            return 0;
+        }
+        if (!p->as) {
+            int lo = 0, hi = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+            HIPCHK(hipStreamCreateWithPriority(&p->as, hipStreamNonBlocking, lo));
+            HIPCHK(hipEventCreateWithFlags(&p->ev_acq, hipEventDisableTiming));
+            HIPCHK(hipMalloc((void **)&p->acq_jobs_d, sizeof(AcqJob) * p->S));
+            HIPCHK(hipMalloc((void **)&p->acq_res_d, sizeof(AcqResult) * p->S));
+            HIPCHK(hipHostMalloc((void **)&p->h_acq, sizeof(AcqResult) * p->S, hipHostMallocDefault));
+            HIPCHK(hipHostMalloc((void **)&p->h_acq_jobs, sizeof(AcqJob) * p->S, hipHostMallocDefault));
+            p->acquiring.assign(p->S, 0);
+        }
+        p->acq_async = true;
         return 0;
     }
     for (int s = (stream < 0 ? 0 : stream); s < (stream < 0 ? p->S : stream + 1); s++) {
@@ -1761,6 +1881,22 @@ int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft, int32_t *ring) {
 int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot) {
     if (!p || !slot || frame < 0 || frame >= p->F) return fail(DABGPU_E_ARG, "bad args");
     *slot = p->last_frames.empty() ? -1 : p->last_frames[frame].out_slot;
+    return 0;
+}
+int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on) {
+    if (!p) return fail(DABGPU_E_ARG, "bad args");
+    p->packed = on != 0;
+    return 0;
+}
+int dabgpu_pipe_fetch(dabgpu_pipe *p, void *dst_h, const void *src_d, size_t bytes) {
+    if (!p || (bytes && (!dst_h || !src_d))) return fail(DABGPU_E_ARG, "bad args");
+    if (p->run_idx == 0) return fail(DABGPU_E_STATE, "no dabgpu_pipe_run to fetch from");
+    if (!bytes) return 0;
+    // on the last run's back-end stream, behind its channel decoding (and DAB+ layer);
+    // the run after next waits for it with the rest of that back end
+    hipStream_t bs = p->vs[p->cur];
+    HIPCHK(hipMemcpyAsync(dst_h, src_d, bytes, hipMemcpyDeviceToHost, bs));
+    HIPCHK(hipEventRecord(p->ev_back[p->cur], bs));
     return 0;
 }
 int dabgpu_pipe_set_display(dabgpu_pipe *p, int on) {

@@ -203,7 +203,8 @@ __device__ __forceinline__ uint32_t window_byte(const DpJob &J, const uint8_t *c
                                                 int nbytes, int cl, int p) {
     const int b = p / nbytes, w = p - b * nbytes, q = cl - 4 + b;
     if (q < 0) return carry[(q + 4) * nbytes + w];
-    return pack_byte(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride, w);
+    const uint8_t *src = J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride;
+    return J.packed ? src[w] : pack_byte(src, w);
 }
 
 // a * b in GF(2)[x] / (x^16 + x^12 + x^5 + 1)
@@ -451,8 +452,8 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
     uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
     for (int p = lane; p < 4 * nbytes; p += 64) {
         const int b = p / nbytes, w = p - b * nbytes, q = nd - 4 + b;
-        nc[p] = q >= 0 ? (uint8_t)pack_byte(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride, w)
-                       : carry[(q + 4) * nbytes + w];
+        const uint8_t *src = J.msc + (((int64_t)stream * J.ncif + (q >= 0 ? q : 0)) * J.nsub + sub) * J.msc_stride;
+        nc[p] = q >= 0 ? (J.packed ? src[w] : (uint8_t)pack_byte(src, w)) : carry[(q + 4) * nbytes + w];
     }
     wave_sync();
     for (int p = lane; p < 4 * nbytes; p += 64) carry[p] = nc[p];

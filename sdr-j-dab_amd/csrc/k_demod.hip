@@ -346,17 +346,18 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                                                     DemodAux aux) {
     __shared__ __attribute__((aligned(16))) float2 ex[EXN];
     // the soft-bit stage and the FreqCorr partials reuse the FFT exchange buffer (after
-    // the FFT's last LDS pass, behind a barrier): 40 KB per workgroup with the NCO
-    // tables, so 4 workgroups per CU
+    // the FFT's last LDS pass, behind a barrier): 34 KB per workgroup
     uint32_t *st = (uint32_t *)ex;
     static_assert(STG * 4 <= sizeof(ex), "stage fits the exchange buffer");
     float2 *fcw = ex;
     __shared__ TwLds twl;
     __shared__ RedLds red;
     const int t = threadIdx.x;
-    __shared__ double2 ncl[GEN ? NCO_USED : 1];
+    // the NCO factor tables are read from global memory (6 KB, cache-resident): the symbol
+    // loop's recurrences need them only at a chunk's start, and 6 KB less LDS per workgroup
+    // (34 KB) leaves room on a CU beside four workgroups for a traceback wave
+    const double2 *ncl = T.nco;
     const DemodTw tw = tw_setup(twl, T, t);
-    nco_setup<GEN>(ncl, T, t);
     __syncthreads();
     const int item = blockIdx.x;
     const int fi = item / nchunks, ch = item % nchunks;

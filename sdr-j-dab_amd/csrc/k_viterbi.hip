@@ -733,7 +733,10 @@ constexpr int TB_ROW = 65;
 // chunk and register ring for two waves per SIMD: measured slower, 0.41 vs 0.37 ms)
 constexpr int TB_CW = 64;
 constexpr int TB_LD = TB_CW / 4;            // 16-byte loads per lane per chunk
-constexpr int TB_RING = 3;                  // decision chunks in the register ring (4 and 5 measured
+#ifndef TB_RING_DEPTH
+#define TB_RING_DEPTH 3
+#endif
+constexpr int TB_RING = TB_RING_DEPTH;      // decision chunks in the register ring (4 and 5 measured
                                            // no faster, profiles/r02_acs_ab.txt -- the compiler waits
                                            // vmcnt(0) at each staging anyway)
 constexpr int TB_WORDS = TB_CW * TB_ROW;    // one chunk of a wave's codewords
@@ -818,9 +821,40 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
 #pragma unroll
     for (int i = 0; i < TB_GROUP; i++) gb[i] = 0;
     const bool al16 = (((uintptr_t)J.out | (uintptr_t)J.out_stride) & 15) == 0;
+    const bool al2 = (((uintptr_t)J.out | (uintptr_t)J.out_stride) & 1) == 0;
+    // packed output: bits t .. t+15 as two bytes, msb first (mp4processor.cpp:115-121's
+    // packing), in one 16-bit store (little-endian: byte t/8 in the low half)
+    auto pk16 = [](uint32_t x) {                           // x: bit k = decoded bit t + k
+        const uint32_t r = __builtin_bitreverse32(x) >> 16;   // bit 15 - k = bit t + k
+        return (r >> 8) | ((r & 0xFFu) << 8);
+    };
     auto flush = [&](int g) {
         const int tg = WS * TB_GROUP * g;
         if (!act || tg >= N) return;
+        if (J.packed) {                                  // 240 bits = 30 bytes at byte tg / 8
+            uint8_t *ob = out + tg / 8;
+            if (al2 && tg + WS * TB_GROUP <= N) {
+#pragma unroll
+                for (int q = 0; q < WS * TB_GROUP / 16; q++) {
+                    const int b = 16 * q, c = b / WS, r = b % WS;              // compile-time
+                    uint32_t x = gb[c] >> r;
+                    if (r > WS - 16) x |= gb[c + 1] << (WS - r);
+                    *(uint16_t *)(ob + 2 * q) = (uint16_t)pk16(x & 0xFFFFu);
+                }
+            } else {                                     // N is a multiple of 8 (24 bitRate, 768)
+                const int nb = min(WS * TB_GROUP, N - tg) / 8;
+#pragma unroll
+                for (int q = 0; q < WS * TB_GROUP / 8; q++) {
+                    const int b = 8 * q, c = b / WS, r = b % WS;                // compile-time
+                    if (q < nb) {
+                        uint32_t x = gb[c] >> r;
+                        if (r > WS - 8) x |= gb[c + 1] << (WS - r);
+                        ob[q] = (uint8_t)(__builtin_bitreverse32(x & 0xFFu) >> 24);
+                    }
+                }
+            }
+            return;
+        }
         if (al16 && tg + WS * TB_GROUP <= N) {
 #pragma unroll
             for (int q = 0; q < WS * TB_GROUP / 16; q++) {

@@ -61,7 +61,7 @@ class StreamState(C.Structure):
                 ("fine", C.c_int16), ("f2correction", C.c_int16), ("prev1", C.c_int16), ("prev2", C.c_int16),
                 ("synced", C.c_int32), ("cif_count", C.c_int64), ("last_start_index", C.c_int32),
                 ("resyncs", C.c_int32), ("acquisitions", C.c_int32), ("attempts", C.c_int32),
-                ("no_signal", C.c_int32), ("frames_run", C.c_int32), ("reserved", C.c_int32)]
+                ("no_signal", C.c_int32), ("frames_run", C.c_int32), ("acquiring", C.c_int32)]
 
 
 class FrameInfo(C.Structure):
@@ -72,6 +72,7 @@ class FrameInfo(C.Structure):
 
 
 CTL_RESET, CTL_COARSE_ON, CTL_COARSE_OFF, CTL_SCAN_ON, CTL_SCAN_OFF, CTL_RESYNC = 1, 2, 3, 4, 5, 6
+CTL_ACQ_ASYNC, CTL_ACQ_SYNC, CTL_INJECT_BOUNDS = 7, 8, 9
 
 
 _lib: Optional[C.CDLL] = None
@@ -123,6 +124,10 @@ def lib() -> C.CDLL:
             "dabgpu_pipe_frame_slot": ([vp, i32, C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frames": ([vp, vp, vp], i32),
             "dabgpu_pipe_set_display": ([vp, i32], i32),
+            "dabgpu_pipe_set_packed": ([vp, i32], i32),
+            "dabgpu_pipe_fetch": ([vp, vp, vp, sz], i32),
+            "dabgpu_host_alloc": ([vp, sz, C.POINTER(vp)], i32),
+            "dabgpu_host_free": ([vp, vp], i32),
             "dabgpu_pipe_iq_display": ([vp, i32, i32, vp], i32),
             "dabgpu_pipe_set_profiling": ([vp, i32], i32),
             "dabgpu_pipe_timing": ([vp, vp, vp], i32),
@@ -264,6 +269,28 @@ class DevBuf:
     def free(self) -> None:
         if self.ptr:
             lib().dabgpu_free(self.ctx.h, self.ptr)
+            self.ptr = None
+
+
+class HostBuf:
+    """page-locked host memory (dabgpu_host_alloc): the target of Pipeline.fetch"""
+
+    def __init__(self, ctx: "Context", nbytes: int):
+        self.ctx, self.nbytes = ctx, int(nbytes)
+        p = C.c_void_p()
+        _chk(lib().dabgpu_host_alloc(ctx.h, max(self.nbytes, 16), C.byref(p)), "dabgpu_host_alloc")
+        self.ptr = p
+
+    def view(self, dtype, shape, offset: int = 0) -> np.ndarray:
+        """a numpy view of the memory (valid until free)"""
+        n = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        assert offset + n <= self.nbytes
+        raw = (C.c_uint8 * n).from_address(self.ptr.value + offset)
+        return np.frombuffer(raw, dtype=dtype).reshape(shape)
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().dabgpu_host_free(self.ctx.h, self.ptr)
             self.ptr = None
 
 
@@ -492,6 +519,8 @@ class Pipeline:
         self.h = h
         self.msc_stride = max([24 * s.bitRate for s in self.subch] + [768])
         self.msc_stride = (self.msc_stride + 15) // 16 * 16
+        self.msc_stride_packed = self.msc_stride // 8        # bytes per codeword with set_packed
+        self.packed = False
         # consecutive runs decode concurrently on two back-end streams (dabgpu.h,
         # dabgpu_pipe_sync): outputs alternate between two buffer sets
         self._outs = [(ctx.buf(n_streams * n_frames * 4 * 768), ctx.buf(n_streams * n_frames * 12),
@@ -502,9 +531,11 @@ class Pipeline:
         self.dp = [s for s in self.subch if s.flags & SUBCH_DABPLUS]
         self.sf_stride = max([110 * (s.bitRate // 8) for s in self.dp] + [16])
         if self.dp:
+            # two sets as well: run r's records may still be copied out (fetch) while
+            # run r+1's DAB+ layer writes
             nrec = n_streams * 4 * n_frames * len(self.dp)
-            self.sf_d = ctx.buf(nrec * self.sf_stride)
-            self.sfi_d = ctx.buf(nrec * C.sizeof(Superframe))
+            self._sf = [(ctx.buf(nrec * self.sf_stride), ctx.buf(nrec * C.sizeof(Superframe))) for _ in range(2)]
+            self.sf_d, self.sfi_d = self._sf[0]
 
     def acquire(self, iq: DevBuf, stride: int, start: Sequence[int], n_avail: Sequence[int]) -> None:
         st = np.asarray(start, dtype=np.int64)
@@ -518,8 +549,9 @@ class Pipeline:
         valid = np.zeros((self.S, 4 * self.F), dtype=np.uint8)
         self.fic_d, self.crc_d, self.msc_d = self._outs[self._run & 1]
         self._run += 1
+        ms = self.msc_stride_packed if self.packed else self.msc_stride
         rc = lib().dabgpu_pipe_run(self.h, iq.ptr, stride, _p(na), self.fic_d.ptr, self.crc_d.ptr,
-                                   self.msc_d.ptr if self.subch else None, self.msc_stride, _p(valid))
+                                   self.msc_d.ptr if self.subch else None, ms, _p(valid))
         if not (partial and rc == -6):
             _chk(rc, "dabgpu_pipe_run")
         if not download:
@@ -527,13 +559,13 @@ class Pipeline:
         self.sync()
         fic = self.fic_d.download(np.uint8, (self.S, self.F, 4, 768))
         crc = self.crc_d.download(np.uint8, (self.S, self.F, 12))
-        msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), self.msc_stride)) \
-            if self.subch else None
+        msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), ms)) if self.subch else None
         return fic, crc, msc, valid
 
     def dabplus(self, download: bool = True):
         """DAB+ superframe layer over the CIFs of the last run() (mp4processor.cpp:107-292).
         Returns (info [S, 4F, n_dabplus] Superframe records, bytes [S, 4F, n_dabplus, sf_stride])."""
+        self.sf_d, self.sfi_d = self._sf[(self._run - 1) & 1]
         _chk(lib().dabgpu_pipe_dabplus(self.h, self.sf_d.ptr, self.sf_stride, self.sfi_d.ptr), "dabgpu_pipe_dabplus")
         if not download:
             return None
@@ -588,6 +620,19 @@ class Pipeline:
         _chk(lib().dabgpu_pipe_frames(self.h, C.cast(fr, C.c_void_p), _p(si)), "dabgpu_pipe_frames")
         return list(fr), si.reshape(self.S, self.F)
 
+    def set_packed(self, on: bool = True) -> None:
+        """MSC output of the following runs: 8 bits per byte, msb first (packbits order)
+        instead of one bit per byte (dabgpu_pipe_set_packed); run() then returns
+        msc [S, 4F, n_subch, msc_stride_packed] bytes"""
+        _chk(lib().dabgpu_pipe_set_packed(self.h, int(on)), "dabgpu_pipe_set_packed")
+        self.packed = bool(on)
+
+    def fetch(self, dst: "HostBuf", src: DevBuf, nbytes: int, dst_off: int = 0) -> None:
+        """asynchronous copy of an output of the last run to pinned host memory, behind
+        that run's channel decoding (dabgpu_pipe_fetch)"""
+        _chk(lib().dabgpu_pipe_fetch(self.h, C.c_void_p(dst.ptr.value + dst_off), src.ptr, nbytes),
+             "dabgpu_pipe_fetch")
+
     def set_display(self, on: bool = True) -> None:
         """keep symbol 2's display carriers of every decoded frame (dabgpu_pipe_set_display)"""
         _chk(lib().dabgpu_pipe_set_display(self.h, int(on)), "dabgpu_pipe_set_display")
@@ -610,7 +655,8 @@ class Pipeline:
 
     def close(self) -> None:
         if self.h:
-            for b in (self.fic_d, self.crc_d, self.msc_d) + ((self.sf_d, self.sfi_d) if self.dp else ()):
-                b.free()
+            for o in self._outs + (self._sf if self.dp else []):
+                for b in o:
+                    b.free()
             lib().dabgpu_pipe_destroy(self.h)
             self.h = None

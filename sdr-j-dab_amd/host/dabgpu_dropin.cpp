@@ -139,10 +139,19 @@ int32_t phaseReference::findIndex(DSPCOMPLEX *v) {
 }
 
 // ---- ficHandler -------------------------------------------------------------------
+// The reference's signals are queued to the GUI thread (Qt); here the FIG parser's
+// events are collected under fibHandling_ and fired after it is released, so a slot may
+// call back into kindofService / dataforAudioService / clearEnsemble without deadlock.
 ficHandler::ficHandler(signals sig, int16_t bitsperBlock) : sig_(std::move(sig)) {
     init(bitsperBlock);
-    fibProcessor_.on_ensemble(sig_.nameofEnsemble);
-    fibProcessor_.on_service(sig_.addtoEnsemble);
+    if (sig_.nameofEnsemble)
+        fibProcessor_.on_ensemble([this](uint32_t id, const std::string &name) {
+            pending_.push_back([this, id, name] { sig_.nameofEnsemble(id, name); });
+        });
+    if (sig_.addtoEnsemble)
+        fibProcessor_.on_service([this](const std::string &label) {
+            pending_.push_back([this, label] { sig_.addtoEnsemble(label); });
+        });
 }
 
 ficHandler::ficHandler(fib_cb cb, int16_t bitsperBlock) : cb_(std::move(cb)) { init(bitsperBlock); }
@@ -172,15 +181,21 @@ void ficHandler::process_ficBlock(int16_t *data, int16_t blkno) {   // fic-handl
             uint8_t bits[768], ok[3];
             bits_.download(bits, 768);
             crc_.download(ok, 3);
+            std::vector<std::function<void()>> events;
             {
                 std::lock_guard<std::mutex> g(fibHandling_);          // fic-handler.cpp:304-320
                 for (int k = 0; k < 3; k++) {
                     total_++;
                     good_ += ok[k] ? 1 : 0;
-                    if (sig_.show_ficCRC) sig_.show_ficCRC(ok[k] != 0);
+                    if (sig_.show_ficCRC) {
+                        const bool b = ok[k] != 0;
+                        pending_.push_back([this, b] { sig_.show_ficCRC(b); });
+                    }
                     if (ok[k]) fibProcessor_.process_FIB(bits + 256 * k, (uint16_t)ficno_);
                 }
+                events.swap(pending_);
             }
+            for (auto &e : events) e();                               // outside the lock
             for (int k = 0; k < 3; k++)
                 if (cb_) cb_(bits + 256 * k, ok[k] != 0, (int16_t)ficno_);
             index_ = 0;

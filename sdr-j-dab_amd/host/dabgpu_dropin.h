@@ -189,6 +189,7 @@ private:
     std::atomic<bool> running_{true};
     std::mutex fibHandling_;
     fib_processor fibProcessor_;
+    std::vector<std::function<void()>> pending_;   // GUI signals raised under fibHandling_, fired after it
     devbuf in_, bits_, crc_;
 };
 

@@ -37,8 +37,8 @@ void mp2Processor::addtoFrame(uint8_t *v, int16_t amount) {         // mp2proces
             addbit(v[i], MP2bitCount_++);
             if (MP2bitCount_ >= lf) {
                 frames_++;
-                if (mp2File_ != nullptr)
-                    (void)std::fwrite(MP2frame_.data(), sizeof(uint8_t), (size_t)lf, mp2File_);   // :581-582
+                if (FILE *f = mp2File_.load())
+                    (void)std::fwrite(MP2frame_.data(), sizeof(uint8_t), (size_t)lf, f);   // :581-582
                 else if (cb_)
                     cb_(MP2frame_.data(), lf, baudRate_);
                 MP2Header_OK_ = 0;

@@ -6,6 +6,7 @@
 // no kjmp2 / faad / MOT / IP handlers -- complete frames and data groups go to
 // callbacks instead.  Same state machines and quirks as the reference.
 #pragma once
+#include <atomic>
 #include <cstdint>
 #include <cstdio>
 #include <functional>
@@ -59,7 +60,7 @@ public:
 private:
     void addbit(uint8_t b, int16_t nm);
     frame_cb cb_;
-    FILE *mp2File_ = nullptr;
+    std::atomic<FILE *> mp2File_{nullptr};   // setFile from the GUI thread, read by the decoding thread
     int32_t baudRate_ = 48000;
     int32_t MP2framesize_;                  // bits
     std::vector<uint8_t> MP2frame_;

@@ -509,6 +509,7 @@ static int gen_core(const dabsynth_cfg *cfg, uint64_t seed, int P, float *iq, ui
         const dabsynth_subch &sc = cfg->subch[s];
         int nb = 24 * sc.bitRate;
         if (cyc && sc.dabplus && NC % 5) return -3;      // superframes must tile the period
+        if (cyc && !sc.dabplus && sc.content == DABSYNTH_PACKET) return -4;   // groups do not wrap (dabsynth.h)
         frag_len[s] = sc.length * 64;
         enc_frag[s].assign((size_t)NE * frag_len[s], 0);
         std::vector<uint8_t> info(nb), mother(4 * (nb + 6)), punct(std::max<size_t>(frag_len[s], mother.size()));
@@ -516,10 +517,39 @@ static int gen_core(const dabsynth_cfg *cfg, uint64_t seed, int P, float *iq, ui
         std::vector<uint8_t> sf(120 * std::max(rsdims, 1));
         // dabplus = 1 + k: the superframe grid is shifted by k CIFs (k = 1..4 makes the
         // receiver's first five CIFs straddle two superframes)
-        int sf_pos = sc.dabplus > 1 ? ((sc.dabplus - 1) % 5) * (nb / 8) : 0;
+        const int shift = sc.dabplus > 1 ? (sc.dabplus - 1) % 5 : 0;
+        int sf_pos = shift * (nb / 8);
         int sf_count = 0;                                 // superframes made (AU layout cycle)
+        // cyclic with a shifted grid: the period's superframes are made on the unshifted
+        // grid (CIF u = 0, 5, 10, ... starts one) and encoder CIF e carries grid CIF
+        // (e + shift) mod 4P, so the superframe straddling the seam is whole
+        std::vector<uint8_t> grid;
+        if (cyc && sc.dabplus && shift) {
+            const int per = nb / 8;
+            grid.resize((size_t)NC * nb);
+            int pos = 0;
+            for (int u = 0; u < NC; u++)
+                for (int byte = 0; byte < per; byte++) {
+                    if (pos == 0) {
+                        int layout = 0;
+                        if (sc.content == DABSYNTH_AU_MIX) {
+                            for (int k = 0; k < 4; k++) {
+                                const int l = (sf_count + k) & 3;
+                                if (superframe_layout_ok(rsdims, l)) { layout = l; break; }
+                            }
+                            sf_count++;
+                        }
+                        make_superframe(rng, rsdims, sf.data(), layout);
+                    }
+                    const uint8_t v = sf[pos];
+                    for (int b = 0; b < 8; b++) grid[(size_t)u * nb + 8 * byte + b] = (uint8_t)((v >> (7 - b)) & 1);
+                    pos = (pos + 1) % (120 * rsdims);
+                }
+        }
         for (int e = e0; e < NC; e++) {
-            if (sc.dabplus) {
+            if (!grid.empty()) {
+                std::memcpy(info.data(), &grid[(size_t)((e + shift) % NC) * nb], nb);
+            } else if (sc.dabplus) {
                 // 5 CIFs carry one superframe; superframes start at e = e0 + 5m
                 int per = nb / 8;
                 for (int byte = 0; byte < per; byte++) {

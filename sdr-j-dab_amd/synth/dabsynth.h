@@ -80,7 +80,9 @@ int dabsynth_generate_many(const dabsynth_cfg *cfg, uint64_t seed0, int n_ens, i
  * stream anywhere.  A stream of any length with the linear generator's layout (frame 0
  * at TF - pre_offset) is iq_stream[p] = iq[(p - (TF - pre_offset)) mod (P * TF)].
  * Truth: fic_bits [P][4][768] by frame; msc_bits [4P][n_subch][24*max_bitRate] by
- * receiver CIF n mod 4P (receiver CIF n decodes encoder CIF (n - 15) mod 4P). */
+ * receiver CIF n mod 4P (receiver CIF n decodes encoder CIF (n - 15) mod 4P).
+ * DABSYNTH_PACKET subchannels are refused (-4): a data group in flight and the packet
+ * continuity counter would not wrap at the seam. */
 int dabsynth_generate_period(const dabsynth_cfg *cfg, uint64_t seed, int period, float *iq,
                              uint8_t *fic_bits, uint8_t *msc_bits);
 /* periods of n_ens ensembles (seeds seed0 + e) in parallel: iq [n_ens][2 * period * TF] */

@@ -3,12 +3,15 @@ ABI) over whole synthetic streams and compare every committed frame with the
 oracle's sequential restatement of the reference CPU path (oracle_py.decode_stream):
 frame placement and correctors, int16 soft bits, FIC bits + CRCs, MSC bits, DAB+
 superframes.  Used by the -m gpu tests and by bench.py's checked step."""
+import time
+
 import numpy as np
 
 import oracle_py as orc
 
 
-def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=(), dabplus=False):
+def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=(), dabplus=False, packed=False,
+               acq_async=False):
     """Decode `runs` x F frames of every stream.  iqs: list of float32 IQ arrays
     (interleaved); n_avail: optional list (per run) of per-stream available sample
     counts.  Returns per stream: dict(info [frames], fic, crc, msc {cif: [nsub][nb]},
@@ -26,12 +29,21 @@ def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=()
                          dabamd.SUBCH_DABPLUS if (len(sc) > 5 and sc[5]) else 0) for sc in subch]
     dpi = [k for k, sc in enumerate(subch) if len(sc) > 5 and sc[5]]
     pipe = dabamd.Pipeline(ctx, S, F, subs, freq_sync_method=method)
+    if packed:                  # MSC bits 8 per byte (dabgpu_pipe_set_packed), unpacked here
+        pipe.set_packed(True)
+    if acq_async:               # null searches in the background (DABGPU_CTL_ACQ_ASYNC) after the first
+        pipe.acquire(diq, stride, [0] * S, lens)
+        pipe.control(dabamd.CTL_ACQ_ASYNC)
     out = [dict(info=[], fic=[], crc=[], msc={}, soft={}, sf={}, states=[]) for _ in range(S)]
     nfr = [0] * S
     try:
         for r in range(runs):
             na = n_avail[r] if n_avail is not None else lens
+            if acq_async and r:
+                time.sleep(0.05)    # a background search finishes between runs (a real-time feed's pace)
             fic, crc, msc, valid = pipe.run(diq, stride, na, partial=True)
+            if packed and msc is not None:
+                msc = np.unpackbits(msc, axis=-1)
             dp = pipe.dabplus() if dpi else None
             fi = pipe.frame_info()
             frames, _ = pipe.frames()

@@ -131,6 +131,41 @@ def test_pipeline_dropout_reacquires_like_reference(ctx):
     assert any(w2 - w1 != 196608 for w1, w2 in zip(wins, wins[1:]))    # the dropout broke the frame grid
 
 
+def test_pipeline_background_reacquisition_like_reference(ctx):
+    """DABGPU_CTL_ACQ_ASYNC: stream 0 loses sync in a dropout (as above); its null search
+    runs in the background while stream 1 keeps decoding n_frames per run, and the runs
+    after the search continue stream 0 from the null it found -- both streams' frames
+    (placement, FIC, MSC, soft bits) equal the oracle's ofdmProcessor::run frame for frame,
+    stream 0's delivered later"""
+    from dabamd.synth import Ensemble
+    sub = MIXED[:2]
+    F, runs = 4, 7
+    e = Ensemble(F * runs + 4, subch=sub, snr_db=20.0)
+    g0, g1 = e.generate(51, truth=False), e.generate(52, truth=False)
+    iq = g0["iq"].reshape(-1, 2).copy()
+    a = g0["frame0"] + 3 * 196608 + 40000
+    b = a + 300000
+    level = float(np.sqrt((iq[:200000] ** 2).sum(1).mean()))
+    ph = 2 * np.pi * 100e3 / 2048000 * np.arange(b - a)
+    rng = np.random.default_rng(5)
+    iq[a:b, 0] = level * np.cos(ph) + rng.normal(0, level / 10, b - a)
+    iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
+    iqs = [np.ascontiguousarray(iq.reshape(-1)), g1["iq"]]
+    refs = orc.decode_streams(iqs, F * runs, sub)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), acq_async=True)
+    runs0 = [(x.frames_run, x.acquiring, x.resyncs) for x in gpu[0]["states"]]
+    print("background re-acquisition:", runs0)
+    assert all(x.frames_run == F for x in gpu[1]["states"])          # stream 1 never waits
+    assert any(fr < F for fr, _, _ in runs0) and any(acq for _, acq, _ in runs0)
+    assert gpu[0]["states"][-1].resyncs >= 1 and gpu[0]["states"][-1].acquisitions >= 2
+    for s in range(2):
+        st = pc.compare(gpu[s], refs[s], sub)
+        print("stream", s, st)
+        _check([st], ("background", s))
+    st0 = pc.compare(gpu[0], refs[0], sub)
+    assert st0["frames"] > 4                   # frames after the dropout were decoded too
+
+
 def test_pipeline_streams_out_of_lockstep(ctx):
     """stream 1 gets fewer samples in run 1 (it commits fewer frames, DABGPU_E_STATE),
     then all of them: its CIF count, 16-CIF de-interleaver and warm-up follow its own
@@ -185,6 +220,29 @@ def test_c5_full_size_superframes_match_reference_path(ctx):
         n, bad, ok3 = n + a, bad + b, ok3 + c
     print("C5 superframe records:", n, "mismatches:", bad, "decoded:", ok3)
     assert bad == 0 and ok3 > 0
+
+
+@pytest.mark.parametrize("packed", [True])
+def test_packed_msc_output_and_dabplus_match_reference_path(ctx, packed):
+    """dabgpu_pipe_set_packed: the traceback writes the MSC bits 8 per byte (msb first,
+    mp4processor.cpp:115-121's packing) and the DAB+ layer reads those bytes -- FIC, MSC
+    and every superframe record equal the reference path, with UEP/EEP and DAB+
+    subchannels side by side, near the decoding threshold"""
+    sub = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 1), (144, 24, 32, 0o104, 0, 0), (168, 36, 48, 0o103, 0, 1),
+           (768, 96, 128, 3, 1, 0)]
+    F, runs = 4, 5
+    iqs = _gen(sub, F * runs + 1, [61, 62], 11.0)
+    refs = orc.decode_streams(iqs, F * runs, sub)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True, packed=packed)
+    ok3 = 0
+    for s in range(2):
+        st = pc.compare(gpu[s], refs[s], sub, check_soft=False)
+        _check([st], ("packed", s), soft=False)
+        assert st["msc_cw"] == len(sub) * (4 * st["frames"] - 16)
+        n, bad, c = pc.compare_dabplus(gpu[s], refs[s], sub)
+        assert bad == 0, (s, n, bad)
+        ok3 += c
+    assert ok3 > 0
 
 
 def _profile_mix():
@@ -339,3 +397,40 @@ def test_pipeline_iq_display_matches_reference_feed(ctx):
         err = np.abs(got[int(fidx)] - want).max() / rms
         print("frame", fidx, "max |gpu - oracle| / rms", err)
         assert err <= 1e-5, (fidx, err)
+
+
+def test_pipeline_back_end_bounds_error_reported_once(ctx):
+    """the back-end streams' error path: an MSC job handed a subchannel offset
+    past the soft-bit ring (DABGPU_CTL_INJECT_BOUNDS) is refused by the Viterbi loader; the
+    pipeline reports DABGPU_E_BOUNDS exactly once (at dabgpu_pipe_sync), and the next run
+    and sync succeed with correct FIC/MSC bits"""
+    import dabamd
+    sub = MIXED[:2]
+    F = 2
+    iqs = _gen(sub, 3 * F + 1, [71], 30.0)
+    ref = orc.decode_stream(iqs[0], 3 * F, sub)
+    diq = ctx.put(iqs[0][None, :])
+    subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, 0) for s in sub]
+    pipe = dabamd.Pipeline(ctx, 1, F, subs)
+    n = len(iqs[0]) // 2
+    try:
+        pipe.run(diq, n, [n])                          # clean
+        pipe.control(dabamd.CTL_INJECT_BOUNDS)
+        pipe.run(diq, n, [n], download=False)          # the faulty back end runs behind this call
+        with pytest.raises(dabamd.DabError, match="out-of-bounds"):
+            pipe.sync()
+        pipe.sync()                                    # reported once
+        fic, crc, msc, valid = pipe.run(diq, n, [n])   # and the pipeline goes on
+        pipe.sync()
+        st = pipe.state(0)
+        cif0 = st.cif_count - 4 * st.frames_run
+        assert st.frames_run == F and crc.all()
+        for c in range(4 * F):
+            if valid[0, c]:
+                for k, sc in enumerate(sub):
+                    nb = 24 * sc[2]
+                    assert np.array_equal(msc[0, c, k, :nb], ref["msc"][cif0 + c, k, :nb])
+        ctx.check()
+    finally:
+        pipe.close()
+        diq.free()

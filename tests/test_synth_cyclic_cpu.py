@@ -56,7 +56,11 @@ def test_cyclic_stream_decodes_across_seams(cfo):
     assert checked >= 2 * 20
     mp4 = orc.MP4(SUBCH[0][2])
     st = [mp4.add(ref["msc"][c, 0, :24 * SUBCH[0][2]])["status"] for c in range(max(16, 4 * f0 + 16), 4 * n)]
-    assert st.count(3) >= 4                               # superframes decoded across the seams
+    # superframes decoded across the seams: once in sync, every superframe decodes (the
+    # reference's blocksInBuffer cycle: four 0s then a 3), none fails its fire code or RS
+    first = st.index(3)
+    assert st.count(3) >= 4 and set(st[first:]) <= {0, 3}, st
+    assert all(st[i] == 3 for i in range(first, len(st), 5)), st
 
 
 def test_period_many_matches_single():
@@ -70,3 +74,12 @@ def test_cyclic_dabplus_needs_whole_superframes():
     ens = Ensemble(4, subch=SUBCH[:1])
     with pytest.raises(Exception):
         ens.generate_period(1, 6)                         # 24 CIFs: not a multiple of 5
+
+
+def test_cyclic_refuses_packet_mode():
+    """packet-mode content does not wrap at the period seam (a data group in flight, the
+    continuity counter): generate_period refuses it rather than make an invalid stream"""
+    from dabamd.synth import PACKET
+    ens = Ensemble(4, subch=[(0, 24, 32, 0o103, 0, 0, PACKET)])
+    with pytest.raises(Exception):
+        ens.generate_period(1, 4)
