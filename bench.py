@@ -424,6 +424,10 @@ def main():
                     help="carrier frequency offset of the synthetic IQ (Hz); nonzero by default: a receiver's NCO "
                          "always runs (phase = coarse + fine correction), 0 takes the constant-phase shortcut")
     ap.add_argument("--iq-source", choices=["local", "rccl"], default="local")
+    ap.add_argument("--msc-format", choices=["bits", "packed"], default="bits",
+                    help="MSC output of the timed steps: one bit per byte as the reference's deconvolve delivers it "
+                         "(viterbi.cpp:240-241), or 8 bits per byte (dabgpu_pipe_set_packed; the DAB+ layer reads "
+                         "either)")
     ap.add_argument("--solo-steps", type=int, default=2,
                     help="steps after the timed region with every kernel alone on the device (profiling mode 3): "
                          "per-kernel times without overlap, to name the dominant kernel")
@@ -495,6 +499,8 @@ def main():
     subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, dabamd.SUBCH_DABPLUS if s[5] else 0)
             for s in SUBCH]
     pipe = dabamd.Pipeline(ctx, E, F, subs)
+    if args.msc_format == "packed":
+        pipe.set_packed(True)
 
     # stream split over RCCL: chunk k of every stream from rank 0 to each rank, converted
     # into this rank's cf32 stream buffer on the GPU
@@ -562,6 +568,8 @@ def main():
     ck = args.warmup + args.steps
     st0 = pipe.state(0)
     (fic, crc, msc, valid), dp = step(ck, download=True)
+    if pipe.packed:
+        msc = np.unpackbits(msc, axis=-1)
     # every rank checks its ensemble 0 against the transmitted bits; rank 0 reports all
     st1 = pipe.state(0)
     check = check_step(truth, P, st0, st1, fic, crc, msc, valid, SUBCH)
@@ -654,7 +662,7 @@ def main():
                 + (", int16 .sdr samples scattered from rank 0 over RCCL" if rccl else ""),
         "config": {"workload": wl_desc, "ensembles_per_gpu": E, "frames_per_step": F,
                    "parallelism": f"ensemble-shard x{world}", "iq_source": "rccl-scatter" if rccl else "rank-local",
-                   "cfo_hz": args.cfo},
+                   "cfo_hz": args.cfo, "msc_output": args.msc_format},
         "realtime_ensembles_per_gpu": value / world / RT_SYMBOLS,
         "roofline": roofline,
         "roofline_hbm_demod": roof_hbm,
@@ -747,7 +755,6 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
     crc = h.view(np.uint8, (E, F, 12), n_fic)
     msc = np.unpackbits(h.view(np.uint8, (E, 4 * F, ns, pipe.msc_stride_packed), n_fic + n_crc), axis=-1)
     check = check_step(truth, P, st0, st1, fic, crc, msc, valids[steps & 1], subch)
-    pipe.set_packed(False)
     for b in hb:
         b.free()
     world = dist.get_world_size() if dist is not None else 1

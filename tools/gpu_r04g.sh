@@ -20,3 +20,10 @@ print("delivered", d.get("delivered_symbols_per_s"), json.dumps(d.get("delivered
 print("sync_loss", json.dumps(d.get("sync_loss"))[:1200])
 print("alone", d["kernel_ms_per_launch_alone"], "pipe", d["kernel_ms_per_launch"])
 PY
+for fmt in bits packed; do
+  timeout -k 10 300 python3 bench.py --workload c5 --steps 20 --warmup 5 --no-cpu-baseline --delivered-steps 0 \
+      --sync-loss-steps 0 --msc-format $fmt > $O/bench_c5_$fmt.log 2>&1 || { tail -5 $O/bench_c5_$fmt.log; exit 1; }
+  python3 -c "
+import json; d=json.loads([l for l in open('$O/bench_c5_$fmt.log') if l.startswith('{')][-1])
+print('c5 $fmt', d['value']/1e6, d['ms_per_step'], 'pipe', d['kernel_ms_per_launch'], 'alone', d['kernel_ms_per_launch_alone'], d['dabplus_last_step'], d['checked_step']['msc_equal_transmitted'])"
+done
