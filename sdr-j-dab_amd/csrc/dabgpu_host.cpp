@@ -1894,6 +1894,9 @@ int dabgpu_pipe_fetch(dabgpu_pipe *p, void *dst_h, const void *src_d, size_t byt
     if (!bytes) return 0;
     // on the last run's back-end stream, behind its channel decoding (and DAB+ layer);
     // the run after next waits for it with the rest of that back end
+    // (the copy is a blit kernel on this runtime; queued on a high-priority stream of its
+    // own it delivered 10 % less -- it then takes wave slots from the next run's ACS:
+    // profiles/r04_delivered_ab.txt)
     hipStream_t bs = p->vs[p->cur];
     HIPCHK(hipMemcpyAsync(dst_h, src_d, bytes, hipMemcpyDeviceToHost, bs));
     HIPCHK(hipEventRecord(p->ev_back[p->cur], bs));

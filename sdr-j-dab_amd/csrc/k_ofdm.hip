@@ -69,6 +69,9 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
     __shared__ int32_t ev[2];                        // lane 0 -> wave: event kind, sample index in block
     const int lane = threadIdx.x;
     if ((int)blockIdx.x >= n) return;
+    // a latency-bound chain on one lane: first pick on its SIMD, so a search launched while
+    // the pipeline's ACS waves fill the SIMDs (a sync loss) is not starved of issue slots
+    __builtin_amdgcn_s_setprio(3);
     const AcqJob jb = jobs[blockIdx.x];
     const float2 *x = iq + jb.iq_base;
     const int32_t ph = jb.phase;
@@ -84,13 +87,30 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
     for (;;) {
         const int nb = (int)min((int64_t)ACQ_BLK, jb.end - pos);
         if (nb <= 0) break;                          // out of samples: still searching
-        for (int i = lane; i < nb; i += 64) {
-            const int64_t p = pos + i;
-            const float2 t = cmul_exact(x[p], osc[acq_lp(p, a, lpa, ph)]);
-            const float j = jan_abs(t);
-            ja[i] = j;
-            hy[i] = hypotf(t.x, t.y);
-            pj[i] = 0.00001 * (double)j;
+        {
+            // all of the block's loads in flight at once (a loop of dependent-looking
+            // iterations issued them one latency at a time: the sequential walk below then
+            // waited for 16 memory round trips per block)
+            constexpr int R = ACQ_BLK / 64;
+            float2 xs[R], os[R];
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int i = lane + 64 * r;
+                const int64_t p = pos + (i < nb ? i : 0);
+                xs[r] = x[p];
+                os[r] = osc[acq_lp(p, a, lpa, ph)];
+            }
+#pragma unroll
+            for (int r = 0; r < R; r++) {
+                const int i = lane + 64 * r;
+                if (i < nb) {
+                    const float2 t = cmul_exact(xs[r], os[r]);
+                    const float j = jan_abs(t);
+                    ja[i] = j;
+                    hy[i] = hypotf(t.x, t.y);
+                    pj[i] = 0.00001 * (double)j;
+                }
+            }
         }
         __syncthreads();
         if (lane == 0) {
