@@ -424,7 +424,7 @@ def main():
                     help="carrier frequency offset of the synthetic IQ (Hz); nonzero by default: a receiver's NCO "
                          "always runs (phase = coarse + fine correction), 0 takes the constant-phase shortcut")
     ap.add_argument("--iq-source", choices=["local", "rccl"], default="local")
-    ap.add_argument("--msc-format", choices=["bits", "packed"], default="bits",
+    ap.add_argument("--msc-format", choices=["bits", "packed"], default="packed",
                     help="MSC output of the timed steps: one bit per byte as the reference's deconvolve delivers it "
                          "(viterbi.cpp:240-241), or 8 bits per byte (dabgpu_pipe_set_packed; the DAB+ layer reads "
                          "either)")

@@ -8,7 +8,7 @@ OUT=$P/build/variant_$1
 mkdir -p "$OUT" "$P/lib/variants"
 FLAGS="--offload-arch=gfx950 -O3 -std=c++17 -fPIC -w $2"
 for f in k_ofdm.hip k_demod.hip k_viterbi.hip k_dabplus.hip dabgpu_host.cpp; do
-    extra=""; [ "$f" = k_demod.hip ] && extra="-fno-slp-vectorize"    # as the Makefile
+    extra=""; [ "$f" = k_demod.hip ] && extra="${DEMOD_FLAGS--fno-slp-vectorize}"    # as the Makefile (env DEMOD_FLAGS: A/B)
     /opt/rocm/bin/hipcc $FLAGS $extra -x hip -c "$P/csrc/$f" -o "$OUT/$f.o" &
 done
 wait
