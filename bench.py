@@ -635,8 +635,13 @@ def main():
                  "achieved": acs_ops / (acs_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                  "traffic": pmc_traffic(acs_kernel, args.workload),
                  "note": "4 int ops per add-compare-select x 64 states per trellis step; peak = 256 CU x 4 SIMD x "
-                         "32 lanes x 2.4 GHz"}
+                         "32 lanes x 2.4 GHz (the 32-bit rate). Formulation ceiling ~0.6 of it: the exact u16x2 ACS "
+                         "word is 6 VALU per wave-step (2 codeword steps = 512 ops), of which the packed-16, DPP, "
+                         "v_perm and v_bfi ops issue at half rate (profiles/r02_valu_rate.txt), ~24 issue cycles + "
+                         "~2 for the loader: 512 / 26 / 32 = 0.62 at 100 % issue; frac_of_ceiling = frac / 0.62",
+                 "formulation_ceiling_frac": 0.62}
     roof_valu["frac"] = roof_valu["achieved"] / roof_valu["peak"]
+    roof_valu["frac_of_ceiling"] = roof_valu["frac"] / roof_valu["formulation_ceiling_frac"]
     if tm_alone.get(acs_stage):
         roof_valu["ms_per_launch"] = acs_ms
         roof_valu["ms_per_launch_alone"] = tm_alone[acs_stage]

@@ -207,6 +207,54 @@ __device__ __forceinline__ uint32_t window_byte(const DpJob &J, const uint8_t *c
     return J.packed ? src[w] : pack_byte(src, w);
 }
 
+// Bytes 4d .. 4d+3 of the same window as one little-endian word (packed MSC with 4-byte
+// aligned rows: a CIF block is 3 * bitRate bytes, a multiple of 24, so no word straddles two)
+__device__ __forceinline__ uint32_t window_word(const DpJob &J, const uint8_t *carry, int stream, int sub,
+                                                int nbytes, int cl, int d) {
+    const int p = 4 * d, b = p / nbytes, w = p - b * nbytes, q = cl - 4 + b;
+    if (q < 0) return *(const uint32_t *)(carry + (q + 4) * nbytes + w);
+    return *(const uint32_t *)(J.msc + (((int64_t)stream * J.ncif + q) * J.nsub + sub) * J.msc_stride + w);
+}
+__device__ __forceinline__ bool words_ok(const DpJob &J) {
+    return J.packed && (((uintptr_t)J.msc | (uintptr_t)J.msc_stride | (uintptr_t)J.ring) & 3) == 0;
+}
+// the window's fsz bytes into LDS: every load of a lane in flight before its first store
+// (a load-store pair per byte would wait out one memory round trip per byte)
+__device__ __forceinline__ void window_to_lds(const DpJob &J, const uint8_t *carry, int stream, int sub, int nbytes,
+                                              int cl, int fsz, uint8_t *dst, int lane) {
+    if (words_ok(J)) {
+        const int nw = fsz >> 2;                         // fsz = 120 RS: a multiple of 4
+        uint32_t *d32 = (uint32_t *)dst;
+        for (int d0 = 0; d0 < nw; d0 += 8 * 64) {
+            uint32_t v[8];
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int d = d0 + 64 * k + lane;
+                v[k] = d < nw ? window_word(J, carry, stream, sub, nbytes, cl, d) : 0u;
+            }
+#pragma unroll
+            for (int k = 0; k < 8; k++) {
+                const int d = d0 + 64 * k + lane;
+                if (d < nw) d32[d] = v[k];
+            }
+        }
+        return;
+    }
+    for (int p0 = 0; p0 < fsz; p0 += 8 * 64) {
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int p = p0 + 64 * k + lane;
+            v[k] = p < fsz ? window_byte(J, carry, stream, sub, nbytes, cl, p) : 0u;
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int p = p0 + 64 * k + lane;
+            if (p < fsz) dst[p] = (uint8_t)v[k];
+        }
+    }
+}
+
 // a * b in GF(2)[x] / (x^16 + x^12 + x^5 + 1)
 __device__ __forceinline__ uint32_t crc_mulmod(uint32_t a, uint32_t b) {
     uint32_t r = 0;
@@ -249,25 +297,33 @@ __global__ __launch_bounds__(64) void k_dp_fire(DpJob J) {
     for (int i = lane; i < 256; i += 64) fire[i] = tf[i];
     wave_sync();
     const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
-    for (int cl = lane; cl < J.ncif; cl += 64) {
-        uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
-        // a window holding an undelivered CIF (de-interleaver warm-up, or a CIF slot the
-        // stream did not fill in this run) is never evaluated
-        bool ok = !(cl >= J.ncifs[stream] || J.cif0s[stream] + cl - 4 < 16);
-        if (ok) {
-            uint32_t x[11];
+    for (int c0 = 0; c0 < J.ncif; c0 += 64) {              // wave-uniform trip count
+        const int cl = c0 + lane;
+        bool ok = false;
+        if (cl < J.ncif) {
+            // a window holding an undelivered CIF (de-interleaver warm-up, or a CIF slot the
+            // stream did not fill in this run) is never evaluated
+            ok = !(cl >= J.ncifs[stream] || J.cif0s[stream] + cl - 4 < 16);
+            if (ok) {
+                uint32_t x[11];
 #pragma unroll
-            for (int p = 0; p < 11; p++) x[p] = window_byte(J, carry, stream, sub, nbytes, cl, p);
-            ok = fire_ok(x, fire);
+                for (int p = 0; p < 11; p++) x[p] = window_byte(J, carry, stream, sub, nbytes, cl, p);
+                ok = fire_ok(x, fire);
+            }
+            J.code[(int64_t)sd * J.ncif + cl] = ok ? 1 : 0;
         }
-        *code = ok ? 1 : 0;
-        if (ok) J.cand[atomicAdd(J.ncand, 1)] = sd * J.ncif + cl;
+        // one queue reservation per wave (same-address atomics serialise in L2)
+        const uint64_t bal = __ballot(ok);
+        int base = 0;
+        if (lane == 0 && bal) base = atomicAdd(J.ncand, (int)__popcll(bal));
+        base = __shfl(base, 0, 64);
+        if (ok) J.cand[base + __popcll(bal & ((1ull << lane) - 1ull))] = sd * J.ncif + cl;
     }
 }
 
 __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     __shared__ GfTabs g;
-    __shared__ uint8_t sfb[120 * DP_MAX_RS];
+    __shared__ __attribute__((aligned(16))) uint8_t sfb[120 * DP_MAX_RS];
     __shared__ uint32_t syn_s[10 * DP_MAX_RS];
     __shared__ uint8_t rl[64 * 40];
     __shared__ int32_t red[64];
@@ -284,7 +340,7 @@ __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
         const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
         uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
         const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
-        for (int p = lane; p < fsz; p += 64) sfb[p] = (uint8_t)window_byte(J, carry, stream, sub, nbytes, cl, p);
+        window_to_lds(J, carry, stream, sub, nbytes, cl, fsz, sfb, lane);
         for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;
         wave_sync();
         // syndromes S_i = sum_m r_m alpha^(i (119-m)) per column: the Horner sums of
@@ -450,10 +506,21 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
     // ones the older part comes from the previous carry (staged: it is overwritten)
     __shared__ uint8_t nc[4 * 3 * 384];
     uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
-    for (int p = lane; p < 4 * nbytes; p += 64) {
-        const int b = p / nbytes, w = p - b * nbytes, q = nd - 4 + b;
-        const uint8_t *src = J.msc + (((int64_t)stream * J.ncif + (q >= 0 ? q : 0)) * J.nsub + sub) * J.msc_stride;
-        nc[p] = q >= 0 ? (J.packed ? src[w] : (uint8_t)pack_byte(src, w)) : carry[(q + 4) * nbytes + w];
+    for (int p0 = 0; p0 < 4 * nbytes; p0 += 8 * 64) {    // a lane's loads in flight together
+        uint32_t v[8];
+#pragma unroll
+        for (int k = 0; k < 8; k++) {
+            const int p = p0 + 64 * k + lane;
+            v[k] = 0;
+            if (p < 4 * nbytes) {
+                const int b = p / nbytes, w = p - b * nbytes, q = nd - 4 + b;
+                const uint8_t *src = J.msc + (((int64_t)stream * J.ncif + (q >= 0 ? q : 0)) * J.nsub + sub) * J.msc_stride;
+                v[k] = q >= 0 ? (J.packed ? src[w] : pack_byte(src, w)) : carry[(q + 4) * nbytes + w];
+            }
+        }
+#pragma unroll
+        for (int k = 0; k < 8; k++)
+            if (p0 + 64 * k + lane < 4 * nbytes) nc[p0 + 64 * k + lane] = (uint8_t)v[k];
     }
     wave_sync();
     for (int p = lane; p < 4 * nbytes; p += 64) carry[p] = nc[p];
