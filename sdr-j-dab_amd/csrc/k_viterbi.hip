@@ -743,7 +743,7 @@ constexpr int TB_LD = TB_CW / 4;            // 16-byte loads per lane per chunk
 constexpr int TB_RING = TB_RING_DEPTH;      // decision chunks in the register ring (4 and 5 measured
                                            // no faster, profiles/r02_acs_ab.txt -- the compiler waits
                                            // vmcnt(0) at each staging anyway)
-constexpr int TB_WORDS = (TB_DMA ? 2 : 1) * TB_CW * TB_ROW;   // one chunk of a wave's codewords (two: LDS-DMA)
+constexpr int TB_WORDS = (TB_DMA == 1 ? 2 : 1) * TB_CW * TB_ROW;   // one chunk of a wave's codewords (two: LDS-DMA)
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TB_GROUP = 8;                 // chunks per output flush (240 bits per codeword)
 constexpr int TB_PRBS = 1024;              // PRBS words (fic-handler.cpp:100-108: 32768 bits)
@@ -972,6 +972,15 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
         for (int i = 0; i < TB_LD; i++)
             __builtin_amdgcn_global_load_lds((const void *)(src + 256 * i), (void *)(img + 256 * i), 16, 0, 0);
     };
+#if TB_DMA == 2
+    // one image (17 KB per wave): the next chunk's loads start when the walk is done
+    for (int ch = nch - 1; ch >= 0; ch--) {
+        dma(stage, ch);
+        __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
+        asm volatile("" ::: "memory");
+        walk(ch, stage);
+    }
+#else
     uint32_t *const img0 = stage, *const img1 = stage + TB_CW * TB_ROW;
     dma((nch - 1) & 1 ? img1 : img0, nch - 1);
     if (nch >= 2) dma((nch - 2) & 1 ? img1 : img0, nch - 2);
@@ -984,6 +993,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
         walk(ch, img);                                   // ends with wave_sync: its reads are done
         if (ch >= 2) dma(img, ch - 2);
     }
+#endif
 #else
     sfor<0, TB_RING>([&](auto ic) { ld(rr[decltype(ic)::value], nch - 1 - decltype(ic)::value); });
     for (int ch = nch - 1; ch >= 0; ch -= TB_RING) {

@@ -248,7 +248,11 @@ ensembleDecoder::ensembleDecoder(const config &cfg) : cfg_(cfg) {
         }
     }
     ndp_ = (int)dp_index_.size();
-    msc_stride_ = (maxbits + 15) / 16 * 16;
+    // the MSC leaves the GPU packed (8 bits per byte, 1/8 of the bytes over PCIe) and is
+    // unpacked here for the one-bit-per-byte consumers (dab-concurrent.cpp:191)
+    chk(dabgpu_pipe_set_packed(pipe_, 1), "dabgpu_pipe_set_packed");
+    msc_stride_ = ((maxbits + 7) / 8 + 15) / 16 * 16;
+    maxbits_ = maxbits;
     sf_stride_ = std::max(16, 110 * maxrs);
     const size_t SF = (size_t)cfg.n_streams * cfg.n_frames;
     fic_.resize(SF * 4 * 768);
@@ -317,14 +321,17 @@ bool ensembleDecoder::step() {
                 }
         }
     if (NS && msc_cb_) {
-        std::vector<uint8_t> msc((size_t)S * 4 * F * NS * msc_stride_);
+        std::vector<uint8_t> msc((size_t)S * 4 * F * NS * msc_stride_), bits(maxbits_);
         msc_.download(msc.data(), msc.size());
         for (int s = 0; s < S; s++)
             for (int c = 0; c < 4 * F; c++) {
                 if (!valid[(size_t)s * 4 * F + c]) continue;
-                for (int k = 0; k < NS; k++)
-                    msc_cb_(s, 4 * frames_done_[s] + c, k, msc.data() + (((size_t)s * 4 * F + c) * NS + k) * msc_stride_,
-                         24 * cfg_.subch[k].bitRate);
+                for (int k = 0; k < NS; k++) {
+                    const uint8_t *pk = msc.data() + (((size_t)s * 4 * F + c) * NS + k) * msc_stride_;
+                    const int nbits = 24 * cfg_.subch[k].bitRate;
+                    for (int i = 0; i < nbits; i++) bits[i] = (uint8_t)((pk[i >> 3] >> (7 - (i & 7))) & 1);
+                    msc_cb_(s, 4 * frames_done_[s] + c, k, bits.data(), nbits);
+                }
             }
     }
     if (NS && ndp_) {

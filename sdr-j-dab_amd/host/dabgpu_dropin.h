@@ -467,7 +467,7 @@ private:
     devbuf iq_, fic_, crc_, msc_, sf_, sfi_;
     int64_t stride_ = 0;
     std::vector<int64_t> navail_;
-    int msc_stride_ = 0, sf_stride_ = 0, ndp_ = 0;
+    int msc_stride_ = 0, sf_stride_ = 0, ndp_ = 0, maxbits_ = 0;
     std::vector<int> dp_index_;
     std::vector<int64_t> frames_done_;     // frames delivered per stream
     fib_cb fib_cb_;

@@ -9,10 +9,14 @@ export TMPDIR=/tmp
 V=sdr-j-dab_amd/lib/variants/libdabgpu_tbdma.so
 DABGPU_TB_WAVES=256 DABGPU_LIB=$V timeout -k 10 600 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pipeline_oracle.py -m gpu -x -q --timeout 300 --timeout-method thread -k "viterbi or profile or c3_full or c5_full or packed or dabplus or fic or au_layouts" > $O/tests_tbdma.log 2>&1 || { tail -30 $O/tests_tbdma.log; exit 1; }
 tail -2 $O/tests_tbdma.log
-BA="--steps 20 --warmup 5 --no-cpu-baseline --delivered-steps 0 --sync-loss-steps 0"
-for r in 1 2; do for v in cur tbdma tbdma_256 tbdma_512; do
-  L=$V; W=0
-  case $v in cur) L=sdr-j-dab_amd/lib/libdabgpu.so;; tbdma_256) W=256;; tbdma_512) W=512;; esac
+DABGPU_LIB=sdr-j-dab_amd/lib/variants/libdabgpu_tbdma1.so timeout -k 10 300 python3 -u -m pytest tests/test_gpu_parity.py tests/test_gpu_pipeline_oracle.py -m gpu -x -q --timeout 200 --timeout-method thread -k "viterbi or c3_full or packed" > $O/tests_tbdma1.log 2>&1 || { tail -30 $O/tests_tbdma1.log; exit 1; }
+tail -2 $O/tests_tbdma1.log
+timeout -k 10 300 python3 -u -m pytest tests/test_gpu_dropin.py -m gpu -x -q --timeout 200 --timeout-method thread > $O/tests_dropin.log 2>&1 || { tail -30 $O/tests_dropin.log; exit 1; }
+tail -2 $O/tests_dropin.log
+BA="--steps 10 --warmup 3 --no-cpu-baseline --delivered-steps 0 --sync-loss-steps 0"
+for r in 1; do for v in cur tbdma tbdma_256 tbdma_512 tbdma1 tbdma1_256 tbdma1_512; do
+  L=sdr-j-dab_amd/lib/variants/libdabgpu_${v%_*}.so; W=${v#*_}; [ "$W" = "$v" ] && W=0
+  [ $v = cur ] && L=sdr-j-dab_amd/lib/libdabgpu.so
   DABGPU_TB_WAVES=$W DABGPU_LIB=$L timeout -k 10 300 python3 bench.py $BA > $O/c3_${v}_$r.log 2>&1 || { tail -5 $O/c3_${v}_$r.log; exit 1; }
   python3 -c "
 import json; d=json.loads([l for l in open('$O/c3_${v}_$r.log') if l.startswith('{')][-1]); k=d['kernel_ms_per_launch']; a=d['kernel_ms_per_launch_alone']
