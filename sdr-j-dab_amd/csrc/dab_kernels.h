@@ -76,13 +76,6 @@ inline __host__ __device__ int64_t dec_bytes(int n_cw, int nbits) {
 inline __host__ __device__ int64_t dec_word_index(int64_t row, int32_t nch) {
     return ((row >> 6) * nch * 64 + (row & 63)) * 64;
 }
-// column of state-lane `lane`'s word within the row.  With the LDS-DMA traceback the
-// columns are XOR-swizzled by the row (the traceback's LDS image is a straight copy of a
-// chunk, so lanes tracing the same state still read 64 different banks)
-#ifndef TB_DMA
-#define TB_DMA 0
-#endif
-inline __host__ __device__ int dec_col(int lane, int64_t row) { return TB_DMA ? lane ^ (int)(row & 63) : lane; }
 
 // depuncturing profile: up to 4 (L_i, PI_i) segments + the 24-bit PI_X tail
 // (deconvolve.cpp:172-237, fic-handler.cpp:254-288)

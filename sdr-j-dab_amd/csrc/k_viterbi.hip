@@ -451,28 +451,26 @@ __device__ __forceinline__ void acs_word_cw(const uint32_t *const (&rp)[6], uint
 // carries one lane offset register instead of a 64-bit address per lane)
 template <int NP, bool FULL, int U>
 __device__ __forceinline__ void acs_word(const uint32_t *const (&rp)[6], uint32_t (&x)[NP], int nst,
-                                         __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP], int64_t o,
-                                         const int (&vo)[2 * NP]) {
+                                         __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP], int64_t o, int lane) {
     uint32_t cw[2 * NP];
     acs_word_cw<NP, FULL, U>(rp, x, nst, cw);
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++)
         if (rb[k] >= 0)
-            __builtin_amdgcn_raw_buffer_store_b32(cw[k], drs, vo[k], (int)(4 * (rb[k] + o)), 0);
+            __builtin_amdgcn_raw_buffer_store_b32(cw[k], drs, 4 * lane, (int)(4 * (rb[k] + o)), 0);
 }
 // the two words of a tile [t0, t0 + VT)
 template <int NP>
 __device__ __forceinline__ void acs_tile(const uint32_t *const (&rp)[6], uint32_t (&x)[NP], int t0, int steps,
-                                         __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP],
-                                         const int (&vo)[2 * NP]) {
+                                         __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2 * NP], int lane) {
     const int64_t cstride = 64 * 64;                    // words per chunk of a 64-row block
     sfor<0, 2>([&](auto uc) {
         constexpr int u = decltype(uc)::value;
         const int tw = t0 + u * WS;
         if (tw < steps) {
             const int64_t o = (int64_t)(tw / WS) * cstride;
-            if (tw + WS <= steps) acs_word<NP, true, u>(rp, x, WS, drs, rb, o, vo);
-            else acs_word<NP, false, u>(rp, x, steps - tw, drs, rb, o, vo);
+            if (tw + WS <= steps) acs_word<NP, true, u>(rp, x, WS, drs, rb, o, lane);
+            else acs_word<NP, false, u>(rp, x, steps - tw, drs, rb, o, lane);
         }
     });
 }
@@ -517,8 +515,8 @@ constexpr int IN_K = 4;                    // <= 4 * VT inputs per tile: 4 round
 template <int KIND>
 __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2], int prof, const ProfR &P, int steps,
                                              const uint32_t (&row)[6], uint32_t (&x)[1],
-                                             __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2], const int (&vo)[2],
-                                             uint32_t *bm, const int2 *ro2, int lane) {
+                                             __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2], uint32_t *bm,
+                                             const int2 *ro2, int lane) {
     const int frag = __builtin_amdgcn_readfirstlane(J.prof[prof].frag);
     const int ioff = __builtin_amdgcn_readfirstlane(J.prof[prof].inv_off);
     const __amdgpu_buffer_rsrc_t rinv =
@@ -570,7 +568,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         put(t0);
         wave_sync();
         if (t0 + VT < steps) fetch(t0 + VT);
-        acs_tile<1>(rp, x, t0, steps, drs, rb, vo);
+        acs_tile<1>(rp, x, t0, steps, drs, rb, lane);
         wave_sync();
     }
 }
@@ -627,13 +625,11 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     }
     uint32_t x[NP];
     int64_t rb[2 * NP];
-    int vo[2 * NP];
 #pragma unroll
     for (int p = 0; p < NP; p++) x[p] = lane == 0 ? 0u : 0x003F003Fu;   // viterbi.cpp:360-371
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++) {
         rb[k] = c[k].valid ? dec_word_index(c[k].row, J.dec_nch) : -1;
-        vo[k] = 4 * dec_col(lane, c[k].row);               // the word's byte offset in its row
     }
     const int64_t cstride = 64 * 64;                    // words per chunk of a 64-row block
     const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc((void *)J.dec, (short)0, -1, 0x00020000);
@@ -641,7 +637,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         // a pair always shares its profile here: SRC_FIC has one, and an SRC_MSC pair is
         // two consecutive CIFs of one subchannel (ncif = 4F is even)
         static_assert(NP == 1, "input-major loader: one codeword pair per wave");
-        acs_tiles_in<KIND>(J, c, c[0].prof, p0, steps, row, x, drs, rb, vo, bm, L.ro2[0], lane);
+        acs_tiles_in<KIND>(J, c, c[0].prof, p0, steps, row, x, drs, rb, bm, L.ro2[0], lane);
     } else {
     // step-major loader (SRC_MOTHER / SRC_FRAG: a pair may have two profiles)
     // inputs of the next tile are loaded while the current one runs its ACS;
@@ -719,7 +715,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         if (mine) put();
         wave_sync();
         fetch(t0 + VT, mine ? t0 + VT + lane : steps);
-        acs_tile<NP>(rp, x, t0, steps, drs, rb, vo);
+        acs_tile<NP>(rp, x, t0, steps, drs, rb, lane);
         wave_sync();
     }
     }
@@ -732,7 +728,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 // phase of every step are compile-time constants.
 // LDS row per codeword: 64 words + 1 pad, so lanes tracing the same state (equal
 // lr, common when the streams carry similar data) read 64 different banks
-constexpr int TB_ROW = TB_DMA ? 64 : 65;     // (LDS-DMA: a straight copy, columns swizzled by dec_col)
+constexpr int TB_ROW = 65;
 // codewords per traceback wave (32 would leave lanes 32..63 idle and halve each wave's
 // chunk and register ring for two waves per SIMD: measured slower, 0.41 vs 0.37 ms)
 constexpr int TB_CW = 64;
@@ -743,7 +739,7 @@ constexpr int TB_LD = TB_CW / 4;            // 16-byte loads per lane per chunk
 constexpr int TB_RING = TB_RING_DEPTH;      // decision chunks in the register ring (4 and 5 measured
                                            // no faster, profiles/r02_acs_ab.txt -- the compiler waits
                                            // vmcnt(0) at each staging anyway)
-constexpr int TB_WORDS = (TB_DMA == 1 ? 2 : 1) * TB_CW * TB_ROW;   // one chunk of a wave's codewords (two: LDS-DMA)
+constexpr int TB_WORDS = TB_CW * TB_ROW;    // one chunk of a wave's codewords
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 constexpr int TB_GROUP = 8;                 // chunks per output flush (240 bits per codeword)
 constexpr int TB_PRBS = 1024;              // PRBS words (fic-handler.cpp:100-108: 32768 bits)
@@ -883,7 +879,6 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
     // the walk of chunk ch over its staged words
     auto walk = [&](int ch, const uint32_t *cur) {
         const uint32_t *mine = cur + (lane & (TB_CW - 1)) * TB_ROW;   // idle lanes walk a copy
-        const uint32_t sw = TB_DMA ? (uint32_t)(lane & 63) : 0u;          // dec_col
         const int t0 = ch * WS;
         uint32_t w = 0;                                  // decoded bits of the chunk, step t0+k at bit k
         // two steps per LDS round trip: with the word of step k, read both candidate
@@ -897,7 +892,7 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
             for (int k = WS - 1; k >= 1; k -= 2) {
                 const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);   // phase of step t0+k is k % 6
                 const uint32_t b1 = 1u << p1, b2 = 1u << p2;
-                const uint32_t w1 = mine[lr ^ sw], c0 = mine[(lr & ~b1) ^ sw], c1 = mine[(lr | b1) ^ sw];
+                const uint32_t w1 = mine[lr], c0 = mine[lr & ~b1], c1 = mine[lr | b1];
                 const uint32_t m1 = (uint32_t)((int32_t)(w1 << (31 - dpos(k))) >> 31);     // -(decision k)
                 w |= (k >= p1 ? ((uint32_t)lr << (k - p1)) : ((uint32_t)lr >> (p1 - k))) & (1u << k);
                 lr = (int)((m1 & b1) | ((uint32_t)lr & ~b1));
@@ -911,8 +906,8 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
 #pragma unroll
             for (int k = WS - 1; k >= 1; k -= 2) {
                 const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);
-                const uint32_t w1 = mine[lr ^ sw];
-                const uint32_t c0 = mine[(lr & ~(1 << p1)) ^ sw], c1 = mine[(lr | (1 << p1)) ^ sw];
+                const uint32_t w1 = mine[lr];
+                const uint32_t c0 = mine[lr & ~(1 << p1)], c1 = mine[lr | (1 << p1)];
                 {
                     const int d = (int)((w1 >> dpos(k)) & 1u);       // predecessor's msb
                     const int u = (lr >> p1) & 1;                     // decoded bit of step t0 + k
@@ -962,39 +957,6 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
         ld(r, ch - TB_RING);
         walk(ch, stage);
     };
-#if TB_DMA
-    // two LDS images of 16 KB, filled by LDS-DMA (global_load_lds_dwordx4: 16 wave-loads
-    // of 1 KB per chunk, no VGPR staging): chunk ch - 1 lands while chunk ch is walked
-    (void)rr; (void)ld; (void)chunk;
-    auto dma = [&](uint32_t *img, int ch) {
-        const uint32_t *src = blk0 + (int64_t)ch * cstride + 4 * lane;
-#pragma unroll
-        for (int i = 0; i < TB_LD; i++)
-            __builtin_amdgcn_global_load_lds((const void *)(src + 256 * i), (void *)(img + 256 * i), 16, 0, 0);
-    };
-#if TB_DMA == 2
-    // one image (17 KB per wave): the next chunk's loads start when the walk is done
-    for (int ch = nch - 1; ch >= 0; ch--) {
-        dma(stage, ch);
-        __builtin_amdgcn_s_waitcnt(0x0F70);              // vmcnt(0)
-        asm volatile("" ::: "memory");
-        walk(ch, stage);
-    }
-#else
-    uint32_t *const img0 = stage, *const img1 = stage + TB_CW * TB_ROW;
-    dma((nch - 1) & 1 ? img1 : img0, nch - 1);
-    if (nch >= 2) dma((nch - 2) & 1 ? img1 : img0, nch - 2);
-    for (int ch = nch - 1; ch >= 0; ch--) {
-        // chunk ch's 16 loads are older than chunk ch - 1's: at most 16 outstanding
-        if (ch > 0) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16) expcnt(7) lgkmcnt(15)
-        else __builtin_amdgcn_s_waitcnt(0x0F70);         // vmcnt(0)
-        asm volatile("" ::: "memory");                   // the walk's LDS reads stay below the wait
-        uint32_t *const img = ch & 1 ? img1 : img0;
-        walk(ch, img);                                   // ends with wave_sync: its reads are done
-        if (ch >= 2) dma(img, ch - 2);
-    }
-#endif
-#else
     sfor<0, TB_RING>([&](auto ic) { ld(rr[decltype(ic)::value], nch - 1 - decltype(ic)::value); });
     for (int ch = nch - 1; ch >= 0; ch -= TB_RING) {
         sfor<0, TB_RING>([&](auto ic) {
@@ -1002,7 +964,6 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
             if (ch - i >= 0) chunk(rr[i], ch - i);       // wave-uniform
         });
     }
-#endif
 }
 
 template <int KIND>
@@ -1028,13 +989,8 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
 template <int KA, int KB>
 __global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) {
     extern __shared__ uint32_t tb_lds[];
-    // a grid smaller than the blocks (tb_grid_cap) walks them in turn: fewer resident
-    // waves, so the next run's demod keeps workgroup room beside them
-    const int nb = nba + (B.n_cw + TB_CW - 1) / TB_CW;
-    for (int b = blockIdx.x; b < nb; b += gridDim.x) {
-        if (b < nba) tb_body<KA>(A, b, tb_lds, tb_lds + TB_WORDS);
-        else tb_body<KB>(B, b - nba, tb_lds, tb_lds + TB_WORDS);
-    }
+    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, tb_lds, tb_lds + TB_WORDS);
+    else tb_body<KB>(B, blockIdx.x - nba, tb_lds, tb_lds + TB_WORDS);
 }
 static size_t tb_lds_bytes(int nch) { return 4 * (size_t)(TB_WORDS + tb_prbs_words(nch)); }
 
@@ -1114,9 +1070,7 @@ hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) 
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
     const int nba = (a.n_cw + TB_CW - 1) / TB_CW, nbb = (b.n_cw + TB_CW - 1) / TB_CW;
-    static const int cap = [] { const char *e = getenv("DABGPU_TB_WAVES"); return e ? atoi(e) : 0; }();   // A/B knob
-    const int grid = cap > 0 ? min(nba + nbb, cap) : nba + nbb;
-    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(grid), dim3(64),
+    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(nba + nbb), dim3(64),
                        tb_lds_bytes(max(a.dec_nch, b.dec_nch)), st, a, b, nba);
     return hipGetLastError();
 }
