@@ -11,7 +11,7 @@ import oracle_py as orc
 
 
 def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=(), dabplus=False, packed=False,
-               acq_async=False):
+               acq_async=False, packed_pad=0):
     """Decode `runs` x F frames of every stream.  iqs: list of float32 IQ arrays
     (interleaved); n_avail: optional list (per run) of per-stream available sample
     counts.  Returns per stream: dict(info [frames], fic, crc, msc {cif: [nsub][nb]},
@@ -31,6 +31,7 @@ def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=()
     pipe = dabamd.Pipeline(ctx, S, F, subs, freq_sync_method=method)
     if packed:                  # MSC bits 8 per byte (dabgpu_pipe_set_packed), unpacked here
         pipe.set_packed(True)
+        pipe.msc_stride_packed += packed_pad    # a row stride that is not a multiple of 4 bytes
     if acq_async:               # null searches in the background (DABGPU_CTL_ACQ_ASYNC) after the first
         pipe.acquire(diq, stride, [0] * S, lens)
         pipe.control(dabamd.CTL_ACQ_ASYNC)

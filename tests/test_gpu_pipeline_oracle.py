@@ -222,18 +222,21 @@ def test_c5_full_size_superframes_match_reference_path(ctx):
     assert bad == 0 and ok3 > 0
 
 
-@pytest.mark.parametrize("packed", [True])
-def test_packed_msc_output_and_dabplus_match_reference_path(ctx, packed):
+@pytest.mark.parametrize("pad", [0, 1])
+def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad):
     """dabgpu_pipe_set_packed: the traceback writes the MSC bits 8 per byte (msb first,
     mp4processor.cpp:115-121's packing) and the DAB+ layer reads those bytes -- FIC, MSC
     and every superframe record equal the reference path, with UEP/EEP and DAB+
-    subchannels side by side, near the decoding threshold"""
+    subchannels side by side, near the decoding threshold.  pad 1: an odd row stride (the
+    traceback's byte stores instead of 16-bit ones, the DAB+ layer's byte-wise window
+    copy instead of 4-byte loads)"""
+    packed = True
     sub = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 1), (144, 24, 32, 0o104, 0, 0), (168, 36, 48, 0o103, 0, 1),
            (768, 96, 128, 3, 1, 0)]
     F, runs = 4, 5
     iqs = _gen(sub, F * runs + 1, [61, 62], 11.0)
     refs = orc.decode_streams(iqs, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True, packed=packed)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True, packed=packed, packed_pad=pad)
     ok3 = 0
     for s in range(2):
         st = pc.compare(gpu[s], refs[s], sub, check_soft=False)
