@@ -407,8 +407,11 @@ int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on);
 /* Copy bytes from an output buffer of the last dabgpu_pipe_run (or dabgpu_pipe_dabplus)
  * to host memory, asynchronously, behind that run's channel decoding on its back-end
  * stream: the results reach the host while the next run decodes.  Complete after
- * dabgpu_pipe_sync, or once the run after next has started (it waits for this back
- * end).  dst_h should be dabgpu_host_alloc memory (else the copy may synchronise). */
+ * dabgpu_pipe_sync (the run after next does not wait for it; its channel decoding, which
+ * may reuse the output buffers, is queued behind it).  dst_h should be dabgpu_host_alloc
+ * memory: with it (and 16-byte aligned pointers and size) a kernel of a few waves writes
+ * the mapped host buffer directly; other memory goes through the runtime's copy, which
+ * may synchronise. */
 int dabgpu_pipe_fetch(dabgpu_pipe *p, void *dst_h, const void *src_d, size_t bytes);
 int dabgpu_pipe_iq_display(dabgpu_pipe *p, int stream, int frame, float *carriers_h);
 

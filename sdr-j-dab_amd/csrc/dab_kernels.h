@@ -182,6 +182,8 @@ hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n
                            const int32_t *slots = nullptr);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
 hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_t n_values, float *dst);
+// device -> mapped pinned host memory by `wgs` workgroups; src, dst, bytes 16-byte aligned
+hipError_t launch_to_host(hipStream_t st, const void *src, void *dst, size_t bytes, int wgs);
 hipError_t launch_rs(hipStream_t st, const uint8_t *in, int n, const uint8_t *tabs, uint8_t *out, int16_t *ret);
 
 }  // namespace dab

@@ -1786,8 +1786,8 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     HIPCHK(prof_mark(p, DABGPU_STAGE_DABPLUS, false));
     HIPCHK(hipEventRecord(p->ev_dp, bs));
     p->dp_rec = true;
-    // the next-but-one run waits for this too (it only reads the MSC output)
-    HIPCHK(hipEventRecord(p->ev_back[p->cur], bs));
+    // (the run after next does not wait for this: the layer reads this run's MSC output
+    // and CIF counters, which that run's back end overwrites behind it on this stream)
     p->last_msc = nullptr;                     // each run's CIFs enter the superframe layer once
     return 0;
 }
@@ -1892,14 +1892,25 @@ int dabgpu_pipe_fetch(dabgpu_pipe *p, void *dst_h, const void *src_d, size_t byt
     if (!p || (bytes && (!dst_h || !src_d))) return fail(DABGPU_E_ARG, "bad args");
     if (p->run_idx == 0) return fail(DABGPU_E_STATE, "no dabgpu_pipe_run to fetch from");
     if (!bytes) return 0;
-    // on the last run's back-end stream, behind its channel decoding (and DAB+ layer);
-    // the run after next waits for it with the rest of that back end
-    // (the copy is a blit kernel on this runtime; queued on a high-priority stream of its
-    // own it delivered 10 % less -- it then takes wave slots from the next run's ACS:
-    // profiles/r04_delivered_ab.txt)
+    // on the last run's back-end stream, behind its channel decoding (and DAB+ layer)
+    // (the runtime's copy is a blit kernel on this runtime; queued on a high-priority
+    // stream of its own it delivered 10 % less -- it then takes wave slots from the next
+    // run's ACS: profiles/r04_delivered_ab.txt)
     hipStream_t bs = p->vs[p->cur];
-    HIPCHK(hipMemcpyAsync(dst_h, src_d, bytes, hipMemcpyDeviceToHost, bs));
-    HIPCHK(hipEventRecord(p->ev_back[p->cur], bs));
+    // into pinned host memory the device can address (dabgpu_host_alloc), 16-byte
+    // aligned: k_to_host's few waves; otherwise the runtime's copy
+    static const int wgs = [] { const char *e = getenv("DABGPU_D2H_WGS"); return e ? atoi(e) : 4; }();
+    void *dd = nullptr;
+    if (wgs > 0 && !((((uintptr_t)dst_h | (uintptr_t)src_d | bytes) & 15)) &&
+        hipHostGetDevicePointer(&dd, dst_h, 0) == hipSuccess && dd)
+        HIPCHK(launch_to_host(bs, src_d, dd, bytes, wgs));
+    else {
+        (void)hipGetLastError();                  // a refused device-pointer query is not an error here
+        HIPCHK(hipMemcpyAsync(dst_h, src_d, bytes, hipMemcpyDeviceToHost, bs));
+    }
+    // no ev_back record: the copy reads only this run's outputs, which the next run on
+    // this stream (the run after next) overwrites in stream order; the front end of that
+    // run does not wait for it
     return 0;
 }
 int dabgpu_pipe_set_display(dabgpu_pipe *p, int on) {

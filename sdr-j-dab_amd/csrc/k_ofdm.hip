@@ -387,4 +387,30 @@ hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_
     return hipGetLastError();
 }
 
+// ---- device -> pinned host copy (dabgpu_pipe_fetch): a few waves stream 16-byte pieces
+// from HBM straight into the mapped host buffer.  The runtime's copy of a device buffer
+// into pinned memory runs as a blit kernel of many workgroups (rocprofv3:
+// __amd_rocclr_copyBuffer) that take wave slots the next run's ACS holds
+// (profiles/r04_delivered_ab.txt); this one needs `wgs` workgroups in all, and PCIe, not
+// the SIMDs, paces it.  Each thread keeps 4 loads in flight before its stores.
+__global__ __launch_bounds__(256) void k_to_host(const uint4 *__restrict__ src, uint4 *__restrict__ dst, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (; i + 3 * stride < n; i += 4 * stride) {
+        const uint4 a = src[i], b = src[i + stride], c = src[i + 2 * stride], d = src[i + 3 * stride];
+        dst[i] = a;
+        dst[i + stride] = b;
+        dst[i + 2 * stride] = c;
+        dst[i + 3 * stride] = d;
+    }
+    for (; i < n; i += stride) dst[i] = src[i];
+}
+
+hipError_t launch_to_host(hipStream_t st, const void *src, void *dst, size_t bytes, int wgs) {
+    if (!bytes) return hipSuccess;
+    if ((((uintptr_t)src | (uintptr_t)dst | bytes) & 15) || wgs <= 0) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_to_host, dim3(wgs), dim3(256), 0, st, (const uint4 *)src, (uint4 *)dst, (int64_t)(bytes / 16));
+    return hipGetLastError();
+}
+
 }  // namespace dab
