@@ -437,3 +437,49 @@ def test_pipeline_back_end_bounds_error_reported_once(ctx):
     finally:
         pipe.close()
         diq.free()
+
+
+def test_fetch_to_host_equals_download(ctx):
+    """dabgpu_pipe_fetch: a run's FIC bits, CRC flags and packed MSC reach pinned host
+    memory behind its channel decoding -- through k_to_host at a 16-byte aligned offset and
+    through the runtime's copy at an odd one -- equal to a synchronous download of the same
+    device buffers, while the next run decodes"""
+    import dabamd
+    sub = MIXED[:3]
+    F, runs = 4, 4
+    iqs = _gen(sub, F * runs + 1, [71, 72], 20.0)
+    S = len(iqs)
+    lens = [len(x) // 2 for x in iqs]
+    stride = max(lens)
+    buf = np.zeros((S, 2 * stride), np.float32)
+    for s, x in enumerate(iqs):
+        buf[s, :len(x)] = x
+    diq = ctx.put(buf)
+    subs = [dabamd.Subch(sc[0], sc[1], sc[2], sc[3], 0 if sc[4] else 1, 0) for sc in sub]
+    pipe = dabamd.Pipeline(ctx, S, F, subs)
+    pipe.set_packed(True)
+    n_fic, n_crc = S * F * 4 * 768, S * F * 12
+    n_msc = S * 4 * F * len(sub) * pipe.msc_stride_packed
+    total = n_fic + n_crc + n_msc
+    hb = [dabamd.HostBuf(ctx, total + 64) for _ in range(2)]
+    try:
+        for r in range(runs):
+            pipe.run(diq, stride, lens, download=False, partial=True)
+            h, base = hb[r & 1], (1 if r & 1 else 0)          # odd runs: unaligned -> runtime copy
+            o = base
+            for src, n in ((pipe.fic_d, n_fic), (pipe.crc_d, n_crc), (pipe.msc_d, n_msc)):
+                pipe.fetch(h, src, n, o)
+                o += n
+            if r >= 1:                                        # the previous run's copy, after this run's
+                pipe.sync()
+                prev = hb[(r - 1) & 1]
+                pb = 1 if (r - 1) & 1 else 0
+                got = prev.view(np.uint8, (total,), pb).copy()
+                exp = np.concatenate([d.download(np.uint8, (n,)) for d, n in
+                                      ((fic_prev, n_fic), (crc_prev, n_crc), (msc_prev, n_msc))])
+                assert np.array_equal(got, exp), r
+                assert got[:n_fic].any()                      # real decoded bits, not an empty buffer
+            fic_prev, crc_prev, msc_prev = pipe.fic_d, pipe.crc_d, pipe.msc_d
+    finally:
+        for b in hb:
+            b.free()
