@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DABGPU_ABI_VERSION 3
+#define DABGPU_ABI_VERSION 4
 
 /* error codes */
 #define DABGPU_OK          0
@@ -385,9 +385,11 @@ int dabgpu_pipe_sync(dabgpu_pipe *p);
 #define DABGPU_NSTAGE         7
 int dabgpu_pipe_set_profiling(dabgpu_pipe *p, int on);
 int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms /*[DABGPU_NSTAGE]*/, int32_t *launches /*[DABGPU_NSTAGE] or NULL*/);
-/* device soft-bit ring of the last run ([n_streams][ring][75][3072]) and the slot of
- * (stream, frame) in it, for tests */
-int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft_d, int32_t *ring_frames);
+/* device soft-bit ring of the last run ([n_streams][ring][75][3072] bytes) and the slot
+ * of (stream, frame) in it, for tests and the ofdmProcessor drop-in.  Each byte is the
+ * ibits value v of processToken (ofdm-decoder.cpp:188-189, always in -127..127) plus 127:
+ * the Viterbi's branch-metric input itself (viterbi.cpp:230-233), half the bytes of int16. */
+int dabgpu_pipe_softbits(dabgpu_pipe *p, const uint8_t **soft_d, int32_t *ring_frames);
 int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot);
 /* per-frame front-end record of the last run: [n_streams][n_frames] */
 int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *frames_h, int32_t *start_index_h);

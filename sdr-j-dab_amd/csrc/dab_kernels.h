@@ -40,7 +40,13 @@ struct DemodAux {
     float2 *disp;           // optional: [out_slot][K] symbol 2's FFT at bins [0, K/2) and
                             // [T_u-1-K/2, T_u-1) -- the iqBuffer feed of processToken
                             // (ofdm-decoder.cpp:192-206)
+    int32_t ring8;          // soft bits as RING8 bytes (the pipeline's ring), else int16
 };
+// The pipeline's soft-bit ring holds each ibits value v as the byte v + 127: processToken's
+// values are (int16_t)(q * 127.0) with |q| <= 1 (ofdm-decoder.cpp:188-189; a 0/0 gives 0),
+// so v + 127 lies in 0..254, and v + 127 is exactly the Viterbi's branch-metric input
+// (viterbi.cpp:230-233: (int16_t)(v + 127) clamped to 0..255, a no-op on that range).
+constexpr int RING8_BIAS = 127;
 constexpr int KERR_FRAME = 1;      // frame descriptor outside its stream / bad NCO phase
 constexpr int KERR_VITERBI = 2;    // Viterbi source outside its buffer
 
@@ -123,6 +129,7 @@ struct VitJob {
     int32_t packed;                 // out: 8 bits per byte, msb first (else one bit per byte)
     const uint32_t *prbs_words;     // PRBS packed 32 bits per word, bit i = prbs[32w+i]
     const uint8_t *valid;           // optional per-codeword flag: 0 = skip
+    int32_t ring8;                  // SRC_FIC / SRC_MSC: src holds RING8 bytes (v + 127), not int16
     // SRC_MSC / SRC_FIC: inverse depuncturing tables, Profile::frag uint16 mother-code
     // positions per profile at Profile::inv_off (make_inv); null: step-major loader
     const uint16_t *inv;

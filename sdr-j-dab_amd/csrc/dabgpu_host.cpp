@@ -792,7 +792,7 @@ struct dabgpu_pipe {
     bool scan = false;               // scanMode (No_Signal_Found after > 5 attempts)
     std::vector<dabgpu_subch> sub;
     std::vector<StreamSt> st;
-    int16_t *ring = nullptr;         // [S][R][75][3072]
+    uint8_t *ring = nullptr;         // [S][R][75][3072] RING8 bytes (soft bit + 127, dab_kernels.h)
     Profile *prof_d = nullptr;       // [NSUB]
     int32_t *substart_d = nullptr;   // [NSUB]
     dabgpu_frame *frames_d = nullptr;
@@ -988,7 +988,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
         if (rc) return;
         if (hipMalloc(ptr, std::max<size_t>(bytes, 256)) != hipSuccess) rc = fail(DABGPU_E_NOMEM, "pipe alloc %zu", bytes);
     };
-    A((void **)&p->ring, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT);
+    A((void **)&p->ring, (size_t)p->S * p->R * FRAME_SOFT);
     A((void **)&p->prof_d, sizeof(Profile) * profs.size());
     A((void **)&p->substart_d, sizeof(int32_t) * ss.size());
     A((void **)&p->frames_d, sizeof(dabgpu_frame) * SF);
@@ -1069,7 +1069,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
         if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(p->substart_d, ss.data(), sizeof(int32_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(p->inv_d, inv.data(), sizeof(uint16_t) * inv.size(), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemset(p->ring, 0, sizeof(int16_t) * (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
+            hipMemset(p->ring, RING8_BIAS, (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
             rc = fail(DABGPU_E_HIP, "pipe init copy failed");
     }
     if (rc) {
@@ -1294,7 +1294,8 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         aux.disp = p->display ? p->disp_d : nullptr;
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         const int kChunks = demod_chunks(n, 2);
-        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
+        aux.ring8 = 1;
+        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, (int16_t *)p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         // the host's values and the error word straight into pinned memory (no copies)
         HIPCHK(launch_front_publish(c->stream, p->fcpart_d, kChunks, n, (float *)p->fc_d, (float *)p->h_fc, p->si_d,
@@ -1412,7 +1413,8 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         const int kChunks = demod_chunks(n3);
         DemodAux aux{};
         aux.disp = p->display ? p->disp_d : nullptr;
-        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, p->ring, nullptr, p->fcpart_d, general, aux));
+        aux.ring8 = 1;
+        HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, (int16_t *)p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
         HIPCHK(hipMemcpyAsync(fc.data(), p->fc_d, sizeof(float2) * n3, hipMemcpyDeviceToHost, c->stream));
@@ -1543,7 +1545,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         if (fic_bits) {
             JF.kind = SRC_FIC;
             JF.n_cw = 4 * S * F;
-            JF.src = p->ring;
+            JF.src = (const int16_t *)p->ring;
+            JF.ring8 = 1;
             JF.src_len = (int64_t)S * p->R * FRAME_SOFT;
             JF.err = p->berr_d + par;
             JF.slots = slots_d;
@@ -1560,7 +1563,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         if (do_msc) {
             JM.kind = SRC_MSC;
             JM.n_cw = S * 4 * F * p->NSUB;
-            JM.src = p->ring;
+            JM.src = (const int16_t *)p->ring;
+            JM.ring8 = 1;
             JM.src_len = (int64_t)S * p->R * FRAME_SOFT;
             JM.err = p->berr_d + par;
             JM.prof = p->prof_d;
@@ -1872,7 +1876,7 @@ int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op) {
     return 0;
 }
 
-int dabgpu_pipe_softbits(dabgpu_pipe *p, const int16_t **soft, int32_t *ring) {
+int dabgpu_pipe_softbits(dabgpu_pipe *p, const uint8_t **soft, int32_t *ring) {
     if (!p || !soft || !ring) return fail(DABGPU_E_ARG, "bad args");
     *soft = p->ring;
     *ring = p->R;

@@ -51,6 +51,7 @@ __device__ __forceinline__ int32_t nco_add(int32_t x, int32_t d) {
     return x >= INPUT_RATE ? x - INPUT_RATE : x;
 }
 typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
 
 // (int16_t)(q * 127.0) exactly as the reference computes it: q promoted to double
 // (ofdm-decoder.cpp:188-189): 3 instructions (cvt, mul_f64, truncating cvt)
@@ -338,7 +339,7 @@ __device__ __forceinline__ void soft_pair(float2 r1, float ab1, int &ir, int &ii
 // stored as 8-byte re / im groups: output rows stay [3072] = re[1536] | im[1536].
 constexpr int STG = K + DT;                              // + one dump slot per thread
 
-template <bool GEN, bool SYNC>
+template <bool GEN, bool SYNC, bool R8>
 __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2 *__restrict__ iq,
                                                     const dabgpu_frame *__restrict__ frames, int nchunks,
                                                     OfdmTables T, int16_t *__restrict__ soft,
@@ -425,9 +426,17 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         const float2 *fb = s + fr.block0;
         const __amdgpu_buffer_rsrc_t rin =
             __builtin_amdgcn_make_buffer_rsrc((void *)fb, (short)0, (TU + NSYM * TS) * 8, 0x00020000);
-        int16_t *orow = soft + (int64_t)fr.out_slot * NSYM * SYMBITS;
+        // soft-bit rows: int16, or RING8 bytes (v + 127) in the pipeline's ring
+        constexpr int esz = R8 ? 1 : 2;
+        char *orow = (char *)soft + (int64_t)fr.out_slot * NSYM * SYMBITS * esz;
         const __amdgpu_buffer_rsrc_t rout =
-            __builtin_amdgcn_make_buffer_rsrc((void *)orow, (short)0, NSYM * SYMBITS * 2, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void *)orow, (short)0, NSYM * SYMBITS * esz, 0x00020000);
+        // the {re, im} pair of a carrier in the stage: int16 each, + 127 each for RING8
+        auto spair = [&](int ir, int ii) -> uint32_t {
+            const uint32_t v = __builtin_amdgcn_perm((uint32_t)ii, (uint32_t)ir, 0x05040100u);
+            if constexpr (!R8) return v;
+            return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, v) + (u16x2){RING8_BIAS, RING8_BIAS});
+        };
         auto ld = [&](int32_t off) -> float2 {                      // off: byte offset from block 0
             return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0));
         };
@@ -549,7 +558,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 int ir, ii;
                 risky |= (uint32_t)soft_fast(r1, ab1, ir, ii) << k;
                 const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
-                *(uint32_t *)((char *)st + addr) = __builtin_amdgcn_perm((uint32_t)ii, (uint32_t)ir, 0x05040100u);
+                *(uint32_t *)((char *)st + addr) = spair(ir, ii);
             }
             if (risky) {
 #pragma unroll
@@ -558,8 +567,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                         const float2 r1 = cmul_conj_exact(a[k], P[k]);
                         const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                         const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
-                        *(uint32_t *)((char *)st + addr) = __builtin_amdgcn_perm(
-                            (uint32_t)trunc127d(-r1.y / ab1), (uint32_t)trunc127d(-r1.x / ab1), 0x05040100u);
+                        *(uint32_t *)((char *)st + addr) = spair(trunc127d(-r1.x / ab1), trunc127d(-r1.y / ab1));
                     }
                 }
             }
@@ -581,15 +589,25 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             for (int k = 0; k < 8; k++) P[k] = a[k];
             __syncthreads();
             // carriers 4q..4q+3, q < 384: re to row[4q..], im to row[K + 4q..]
-            const int32_t rowb = (l - 1) * SYMBITS * 2;
-            for (int q = t; q < K / 4; q += DT) {
-                const uint4 w = ((const uint4 *)st)[q];
-                const uint2 re = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x05040100u),
-                                            __builtin_amdgcn_perm(w.w, w.z, 0x05040100u));
-                const uint2 im = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x07060302u),
-                                            __builtin_amdgcn_perm(w.w, w.z, 0x07060302u));
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, re), rout, rowb + 8 * q, 0, 0);
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, im), rout, rowb + 2 * K + 8 * q, 0, 0);
+            const int32_t rowb = (l - 1) * SYMBITS * esz;
+            if constexpr (R8) {                        // the low bytes of each half
+                for (int q = t; q < K / 4; q += DT) {
+                    const uint4 w = ((const uint4 *)st)[q];
+                    const uint32_t xy = __builtin_amdgcn_perm(w.y, w.x, 0x06040200u);   // re0 im0 re1 im1
+                    const uint32_t zw = __builtin_amdgcn_perm(w.w, w.z, 0x06040200u);   // re2 im2 re3 im3
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(zw, xy, 0x06040200u), rout, rowb + 4 * q, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(zw, xy, 0x07050301u), rout, rowb + K + 4 * q, 0, 0);
+                }
+            } else {
+                for (int q = t; q < K / 4; q += DT) {
+                    const uint4 w = ((const uint4 *)st)[q];
+                    const uint2 re = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x05040100u),
+                                                __builtin_amdgcn_perm(w.w, w.z, 0x05040100u));
+                    const uint2 im = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x07060302u),
+                                                __builtin_amdgcn_perm(w.w, w.z, 0x07060302u));
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, re), rout, rowb + 8 * q, 0, 0);
+                    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u32, im), rout, rowb + 2 * K + 8 * q, 0, 0);
+                }
             }
             __syncthreads();
         }
@@ -828,13 +846,15 @@ hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr,
     const dim3 grid(n * nchunks), block(DT);
     const float2 *x = (const float2 *)iq;
     float2 *fp = (float2 *)fcpart;
-    if (aux.si) {
-        if (general) hipLaunchKernelGGL((k_demod_wg<true, true>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
-        else hipLaunchKernelGGL((k_demod_wg<false, true>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
+#define DEMOD_GO(G, S, R) hipLaunchKernelGGL((k_demod_wg<G, S, R>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux)
+    if (aux.ring8) {                                   // the pipeline's RING8 ring
+        if (aux.si) { if (general) DEMOD_GO(true, true, true); else DEMOD_GO(false, true, true); }
+        else { if (general) DEMOD_GO(true, false, true); else DEMOD_GO(false, false, true); }
     } else {
-        if (general) hipLaunchKernelGGL((k_demod_wg<true, false>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
-        else hipLaunchKernelGGL((k_demod_wg<false, false>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux);
+        if (aux.si) { if (general) DEMOD_GO(true, true, false); else DEMOD_GO(false, true, false); }
+        else { if (general) DEMOD_GO(true, false, false); else DEMOD_GO(false, false, false); }
     }
+#undef DEMOD_GO
     return hipGetLastError();
 }
 

@@ -74,8 +74,10 @@ struct Src {
 // SRC_MSC logical order (stream, subchannel, CIF) -- consecutive CIFs of one
 // subchannel share 15 of their 16 source rows and their profile; output rows stay
 // ((stream * ncif) + cif) * nsub + sub.
-template <int KIND>
+template <int KIND, bool B8 = false>
 __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *rowoff, int lane) {
+    static_assert(!B8 || KIND == SRC_FIC || KIND == SRC_MSC, "RING8 bytes: the pipeline's ring only");
+    constexpr int ESZ = B8 ? 1 : 2;                    // bytes per soft value
     Src c;
     c.prof = 0;
     c.valid = logical < J.n_cw;
@@ -89,7 +91,8 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
     } else if constexpr (KIND == SRC_FIC) {
         const int32_t slot = J.slots[logical >> 2];    // < 0: frame not committed
         c.valid = c.valid && slot >= 0;
-        c.base = J.src + (int64_t)(slot < 0 ? 0 : slot) * FRAME_SOFT + (logical & 3) * 2304;
+        c.base = (const int16_t *)((const char *)J.src +
+                                   ESZ * ((int64_t)(slot < 0 ? 0 : slot) * FRAME_SOFT + (logical & 3) * 2304));
     } else {
         const int cl = logical % J.ncif;
         const int rest = logical / J.ncif;
@@ -100,7 +103,7 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
         const int64_t cif = J.cif0s[stream] + cl;
         // CIFs the stream delivered in this batch; dab-concurrent.cpp:172-175 warm-up
         c.valid = c.valid && cl < J.ncifs[stream] && cif >= 16;
-        c.base = J.src + (int64_t)stream * J.ring * FRAME_SOFT;
+        c.base = (const int16_t *)((const char *)J.src + ESZ * (int64_t)stream * J.ring * FRAME_SOFT);
         if (lane < 16) {
             // element idx of CIF n comes from CIF n - d[idx & 15] (dab-concurrent.cpp:42-43,162-169)
             const int b = lane;
@@ -126,15 +129,15 @@ __device__ __forceinline__ Src src_of(const VitJob &J, int logical, int32_t *row
         if (c.valid) {
             const Profile &P = J.prof[c.prof];
             const int64_t need = P.nseg ? P.frag : 4 * (int64_t)(P.nbits + 6);
-            const int64_t o = c.base - J.src;
+            const int64_t o = ((const char *)c.base - (const char *)J.src) / ESZ;   // in soft values
             if (o < 0 || o + need > J.src_len) {      // never read outside the buffer
                 if (lane == 0) atomicOr(J.err, KERR_VITERBI);
                 c.valid = false;
             }
-            nrec = 2 * need;
+            nrec = ESZ * need;
         }
     } else {
-        nrec = 2 * (int64_t)J.ring * FRAME_SOFT;        // the stream's ring (rowoff checked above)
+        nrec = ESZ * (int64_t)J.ring * FRAME_SOFT;      // the stream's ring (rowoff checked above)
     }
     // wave-uniform by construction; readfirstlane keeps the descriptor in SGPRs
     const uint64_t b = (uint64_t)(uintptr_t)c.base;
@@ -276,11 +279,16 @@ constexpr uint32_t SPREAD = 6 * 1020;
 // branch metrics of one step for the 8 (b0,b1,b2) output patterns, both codewords
 // (viterbi.cpp:159-164: metric = sum_j sym_j ^ B_j with b3 = b0; y ^ 255 = 255 - y).
 // Every partial sum stays inside its 16-bit half, so plain 32-bit adds work on pairs.
+template <bool B8 = false>
 __device__ __forceinline__ void put_bm(uint32_t *bm, int j, const u16x2 (&s)[4]) {
     typedef short i16x2 __attribute__((ext_vector_type(2)));
     uint32_t y[4];
 #pragma unroll
     for (int e = 0; e < 4; e++) {
+        if constexpr (B8) {                 // RING8 bytes: already v + 127 in 0..254
+            y[e] = as_u32(s[e]);
+            continue;
+        }
         // int16_t temp = input[i] + 127, clamped to 0..255 (viterbi.cpp:230-233): the sum
         // wraps in 16 bits like the reference's int16_t, so inputs above 32640 become 0
         const i16x2 t = __builtin_bit_cast(i16x2, as_u32(s[e] + (u16x2){127, 127}));
@@ -512,7 +520,7 @@ __device__ __forceinline__ int in_index(const ProfR &P, int t) {
 // one step per lane.  The step-major loader below spends ~2.4 VALU instructions per
 // trellis step on the depuncturing and delay-line selects of every value; this one 0.9.
 constexpr int IN_K = 4;                    // <= 4 * VT inputs per tile: 4 rounds of 64 lanes
-template <int KIND>
+template <int KIND, bool B8>
 __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2], int prof, const ProfR &P, int steps,
                                              const uint32_t (&row)[6], uint32_t (&x)[1],
                                              __amdgpu_buffer_rsrc_t drs, const int64_t (&rb)[2], uint32_t *bm,
@@ -531,19 +539,27 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         int2 ro;
         if constexpr (KIND == SRC_MSC) ro = ro2[i & 15];
         else ro = make_int2(c[0].valid ? 0 : RO_EMPTY, c[1].valid ? 0 : RO_EMPTY);
-        const int oa = ro.x + 2 * i, ob = ro.y + 2 * i, oi = 2 * i;
+        constexpr int ESZ = B8 ? 1 : 2;
+        const int oa = ro.x + ESZ * i, ob = ro.y + ESZ * i, oi = 2 * i;
 #pragma unroll
         for (int k = 0; k < IN_K; k++) {
             if (64 * k < I1 - I0) {
-                vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
-                vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);
+                if constexpr (B8) {
+                    vab[k][0] = __builtin_amdgcn_raw_buffer_load_b8(c[0].rs, oa, 64 * k, 0);
+                    vab[k][1] = __builtin_amdgcn_raw_buffer_load_b8(c[1].rs, ob, 64 * k, 0);
+                } else {
+                    vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
+                    vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);
+                }
                 vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
             }
         }
     };
     // the staging table (4 * VT words) aliases the bm rows: it is read before they are written
     auto put = [&](int t0) {
-        if (lane < VT) *(uint4 *)&bm[4 * lane] = make_uint4(0u, 0u, 0u, 0u);
+        // erasures (deconvolve.cpp:182 / fic-handler.cpp:259: soft value 0): 0, or 127 as RING8 bytes
+        constexpr uint32_t E0 = B8 ? 0x007F007Fu : 0u;
+        if (lane < VT) *(uint4 *)&bm[4 * lane] = make_uint4(E0, E0, E0, E0);
         wave_sync();
         const int n = I1 - I0;
 #pragma unroll
@@ -558,7 +574,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         sv[2] = as_pk(q.z);
         sv[3] = as_pk(q.w);
         wave_sync();
-        if (lane < VT) put_bm(bm, lane, sv);
+        if (lane < VT) put_bm<B8>(bm, lane, sv);
     };
     const uint32_t *rp[6];
 #pragma unroll
@@ -573,7 +589,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
     }
 }
 
-template <int KIND, int NP>
+template <int KIND, int NP, bool B8 = false>
 __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) {
     uint32_t *bm = L.bm;
     int32_t (*rowoff)[16] = L.rowoff;
@@ -582,7 +598,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
     bool any = false;
 #pragma unroll
     for (int k = 0; k < 2 * NP; k++) {
-        c[k] = src_of<KIND>(J, 2 * NP * w + k, rowoff[k], lane);
+        c[k] = src_of<KIND, B8>(J, 2 * NP * w + k, rowoff[k], lane);
         any = any || c[k].valid;
     }
     if (!any) return;
@@ -594,8 +610,9 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
 #pragma unroll
             for (int p = 0; p < NP; p++) {
                 const int32_t a = rowoff[2 * p][lane], b = rowoff[2 * p + 1][lane];
-                L.ro2[p][lane] = make_int2(a >= 0 && c[2 * p].valid ? 2 * a : RO_EMPTY,
-                                           b >= 0 && c[2 * p + 1].valid ? 2 * b : RO_EMPTY);
+                constexpr int ESZ = B8 ? 1 : 2;
+                L.ro2[p][lane] = make_int2(a >= 0 && c[2 * p].valid ? ESZ * a : RO_EMPTY,
+                                           b >= 0 && c[2 * p + 1].valid ? ESZ * b : RO_EMPTY);
             }
         }
         wave_sync();
@@ -637,7 +654,7 @@ __device__ __forceinline__ void acs_body(const VitJob &J, int w, AcsLds<NP> &L) 
         // a pair always shares its profile here: SRC_FIC has one, and an SRC_MSC pair is
         // two consecutive CIFs of one subchannel (ncif = 4F is even)
         static_assert(NP == 1, "input-major loader: one codeword pair per wave");
-        acs_tiles_in<KIND>(J, c, c[0].prof, p0, steps, row, x, drs, rb, bm, L.ro2[0], lane);
+        acs_tiles_in<KIND, B8>(J, c, c[0].prof, p0, steps, row, x, drs, rb, bm, L.ro2[0], lane);
     } else {
     // step-major loader (SRC_MOTHER / SRC_FRAG: a pair may have two profiles)
     // inputs of the next tile are loaded while the current one runs its ACS;
@@ -966,19 +983,19 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
     }
 }
 
-template <int KIND>
+template <int KIND, bool B8 = false>
 __global__ __launch_bounds__(64, 8) void k_acs(VitJob J) {
     __shared__ AcsLds<1> L;
-    acs_body<KIND, 1>(J, xcd_order(blockIdx.x, gridDim.x), L);
+    acs_body<KIND, 1, B8>(J, xcd_order(blockIdx.x, gridDim.x), L);
 }
 // two jobs in one launch (the pipeline's MSC and FIC): blocks [0, nwa) run job A,
 // the rest job B, so B's short waves fill the SIMDs A's last waves leave idle
-template <int KA, int KB>
+template <int KA, int KB, bool B8 = false>
 __global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
     __shared__ AcsLds<1> L;
     const int b = blockIdx.x;
-    if (b < nwa) acs_body<KA, 1>(A, xcd_order(b, nwa), L);
-    else acs_body<KB, 1>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
+    if (b < nwa) acs_body<KA, 1, B8>(A, xcd_order(b, nwa), L);
+    else acs_body<KB, 1, B8>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
 }
 // LDS (dynamic): the staging buffer, then tb_prbs_words(dec_nch) PRBS words
 template <int KIND>
@@ -1047,6 +1064,13 @@ template <int KIND> struct TbK { static auto fn() { return k_traceback<KIND>; } 
 hipError_t launch_acs(hipStream_t st, const VitJob &job) {
     if (job.n_cw <= 0) return hipSuccess;
     if (job.dec_ncw < dec_rows(job.n_cw) || job.dec_nch <= 0) return hipErrorInvalidValue;
+    if (job.ring8) {                                   // the pipeline's RING8 soft-bit ring
+        const dim3 grid((job.n_cw + 1) / 2);
+        if (job.kind == SRC_FIC) hipLaunchKernelGGL((k_acs<SRC_FIC, true>), grid, dim3(64), 0, st, job);
+        else if (job.kind == SRC_MSC) hipLaunchKernelGGL((k_acs<SRC_MSC, true>), grid, dim3(64), 0, st, job);
+        else return hipErrorInvalidValue;
+        return hipGetLastError();
+    }
     return launch_kind<AcsK>(st, job, dim3((job.n_cw + 1) / 2));
 }
 hipError_t launch_traceback(hipStream_t st, const VitJob &job) {
@@ -1063,8 +1087,10 @@ hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) 
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
     if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw) || a.dec_nch <= 0 || b.dec_nch <= 0)
         return hipErrorInvalidValue;
+    if (a.ring8 != b.ring8) return hipErrorInvalidValue;
     const int nwa = (a.n_cw + 1) / 2, nwb = (b.n_cw + 1) / 2;
-    hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
+    if (a.ring8) hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC, true>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
+    else hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
     return hipGetLastError();
 }
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {

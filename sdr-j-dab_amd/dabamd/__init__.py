@@ -645,13 +645,14 @@ class Pipeline:
         return out[:, 0] + 1j * out[:, 1]
 
     def softbits(self) -> np.ndarray:
-        """the soft-bit ring of the last run as [stream][slot][75][3072] ibits rows"""
+        """the soft-bit ring of the last run as [stream][slot][75][3072] ibits rows (the ring
+        holds ibits + 127 as bytes, dabgpu.h dabgpu_pipe_softbits)"""
         p, r = C.c_void_p(), C.c_int32()
         _chk(lib().dabgpu_pipe_softbits(self.h, C.byref(p), C.byref(r)), "softbits")
         n = self.S * r.value * NSYM * SYMBITS
-        out = np.empty(n, dtype=np.int16)
-        _chk(lib().dabgpu_memcpy_d2h(self.ctx.h, _p(out), p, out.nbytes), "d2h")
-        return out.reshape(self.S, r.value, NSYM, SYMBITS)
+        raw = np.empty(n, dtype=np.uint8)
+        _chk(lib().dabgpu_memcpy_d2h(self.ctx.h, _p(raw), p, raw.nbytes), "d2h")
+        return (raw.astype(np.int16) - 127).reshape(self.S, r.value, NSYM, SYMBITS)
 
     def close(self) -> None:
         if self.h:

@@ -320,11 +320,12 @@ void ofdmProcessor::run() {                                        // ofdm-proce
     bufs[1].resize(sizeof(float) * 2 * CAP);
     int cur = 0;
     int64_t base = 0, end = 0, last_run = -1;
-    const int16_t *ring = nullptr;
+    const uint8_t *ring = nullptr;                  // RING8 bytes: ibits + 127
     int32_t R = 0;
     chk(dabgpu_pipe_softbits(pipe, &ring, &R), "dabgpu_pipe_softbits");
     std::vector<DSPCOMPLEX> chunk(1 << 16);
     std::vector<int16_t> soft((size_t)75 * 3072);
+    std::vector<uint8_t> soft8(soft.size());
     std::vector<DSPCOMPLEX> carriers(DABGPU_K);
     while (running_) {
         {
@@ -389,8 +390,8 @@ void ofdmProcessor::run() {                                        // ofdm-proce
             chk(dabgpu_pipe_frame_info(pipe, &fi), "dabgpu_pipe_frame_info");
             int32_t slot = 0;
             chk(dabgpu_pipe_frame_slot(pipe, 0, &slot), "dabgpu_pipe_frame_slot");
-            chk(dabgpu_memcpy_d2h(c, soft.data(), ring + (size_t)slot * 75 * 3072, sizeof(int16_t) * soft.size()),
-                "soft bits");
+            chk(dabgpu_memcpy_d2h(c, soft8.data(), ring + (size_t)slot * 75 * 3072, soft8.size()), "soft bits");
+            for (size_t i = 0; i < soft.size(); i++) soft[i] = (int16_t)(soft8[i] - 127);   // processToken's ibits
             // the frame's getSample(s) calls (ofdm-processor.cpp:344-453): the null search and
             // the T_u window one sample at a time, the rest of block 0, 75 symbols, the null
             consume_singles(fi.window + DABGPU_TU, &fi);
