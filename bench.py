@@ -629,7 +629,9 @@ def main():
     acs_ms = max(tm[acs_stage][1], 1e-9)            # average launch duration
     acs_ops = acs_steps * 64 * 4                    # 2 adds + compare + select per ACS
     demod_ms = max(tm["demod"][1], 1e-9)
-    demod_bytes = E * F * (75 * (8 * TS + 2 * 3072) + 8 * TU)   # + the findIndex window
+    # cf32 in + the pipeline's RING8 soft bits out (one byte each: ibits + 127) + the
+    # findIndex window; SURVEY 8(d)'s 26,560 B/symbol counts int16 soft bits out
+    demod_bytes = E * F * (75 * (8 * TS + 3072) + 8 * TU)
     demod_kernel = "dab::k_demod_wg<true, true>" if args.cfo else "dab::k_demod_wg<false, true>"
     roof_valu = {"kernel": f"{acs_kernel[5:]} (Viterbi ACS)", "bound": "valu",
                  "achieved": acs_ops / (acs_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
@@ -649,7 +651,8 @@ def main():
     roof_hbm = {"kernel": f"{demod_kernel[5:]} (findIndex + FFT + DQPSK)", "bound": "hbm",
                 "achieved": demod_bytes / (demod_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "traffic": pmc_traffic(demod_kernel, args.workload), "algorithmic_bytes": demod_bytes,
-                "note": "algorithmic bytes: 8*T_s cf32 in + 2*2K int16 out per data symbol + 8*T_u of the "
+                "note": "algorithmic bytes: 8*T_s cf32 in + 2K soft bits out as RING8 bytes (ibits + 127; "
+                        "SURVEY 8(d)'s 26,560 B/symbol assumes int16 out) per data symbol + 8*T_u of the "
                         "findIndex window per frame"}
     roof_hbm["frac"] = roof_hbm["achieved"] / roof_hbm["peak"]
     if tm_alone.get("demod"):
@@ -681,7 +684,9 @@ def main():
         "acquire_ms": {"streams": E, "ms": acquire_ms, "note": "initial null search of every stream (host-timed, first launch)"},
         # the whole step priced at the front end's algorithmic bytes
         "hbm_frac_step": value / world * SYMBOL_BYTES / (HBM_PEAK_GBS * 1e9),
-        "hbm_frac_step_note": "symbols/s per GPU x 26,560 B (8 T_s cf32 in + 2 x 3072 int16 out per symbol) / 8 TB/s",
+        "hbm_frac_step_note": "BASELINE.md 4.4's definition: symbols/s per GPU x 26,560 B (8 T_s cf32 in + 2 x 3072 "
+                              "int16 out per symbol) / 8 TB/s (the ring now holds the soft bits as bytes: 23,488 B "
+                              "per symbol move)",
     }
     if delivered is not None:
         out["delivered_symbols_per_s"] = delivered.pop("value")
