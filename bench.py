@@ -625,14 +625,14 @@ def main():
     # the pipeline decodes the FIC in the MSC's ACS launch (dabgpu.h, DABGPU_STAGE_FIC)
     acs_steps = E * 4 * F * sum(24 * s[2] + 6 for s in SUBCH) + E * F * 4 * (768 + 6)
     # (without MSC subchannels the FIC has launches of its own, k_acs<2>)
-    acs_stage, acs_kernel = ("msc_acs", "dab::k_acs2<3, 2>") if SUBCH else ("fic", "dab::k_acs<2>")
+    acs_stage, acs_kernel = ("msc_acs", "dab::k_acs2<3, 2, true>") if SUBCH else ("fic", "dab::k_acs<2, true>")
     acs_ms = max(tm[acs_stage][1], 1e-9)            # average launch duration
     acs_ops = acs_steps * 64 * 4                    # 2 adds + compare + select per ACS
     demod_ms = max(tm["demod"][1], 1e-9)
     # cf32 in + the pipeline's RING8 soft bits out (one byte each: ibits + 127) + the
     # findIndex window; SURVEY 8(d)'s 26,560 B/symbol counts int16 soft bits out
     demod_bytes = E * F * (75 * (8 * TS + 3072) + 8 * TU)
-    demod_kernel = "dab::k_demod_wg<true, true>" if args.cfo else "dab::k_demod_wg<false, true>"
+    demod_kernel = "dab::k_demod_wg<true, true, true>" if args.cfo else "dab::k_demod_wg<false, true, true>"
     roof_valu = {"kernel": f"{acs_kernel[5:]} (Viterbi ACS)", "bound": "valu",
                  "achieved": acs_ops / (acs_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                  "traffic": pmc_traffic(acs_kernel, args.workload),
