@@ -73,6 +73,9 @@ struct AcqResult {
 // contiguous: dec[((row / 64 * dec_nch + chunk) * 64 + row % 64) * 64 + lane]
 // (dec_word_index); rows padded to a whole block of 64
 constexpr int DEC_WORD_STEPS = 30;
+// mother-code positions (4 per trellis step) of one ACS branch-metric tile (two decision
+// words, 60 steps): the inverse depuncturing tables hold positions within their tile
+constexpr int VIT_TILE_POS = 4 * 2 * DEC_WORD_STEPS;
 inline __host__ __device__ int64_t dec_rows(int n_cw) { return ((int64_t)n_cw + 63) / 64 * 64; }
 inline __host__ __device__ int32_t dec_chunks(int nbits) { return (nbits + 6 + DEC_WORD_STEPS - 1) / DEC_WORD_STEPS; }
 inline __host__ __device__ int64_t dec_bytes(int n_cw, int nbits) {
@@ -130,9 +133,10 @@ struct VitJob {
     const uint32_t *prbs_words;     // PRBS packed 32 bits per word, bit i = prbs[32w+i]
     const uint8_t *valid;           // optional per-codeword flag: 0 = skip
     int32_t ring8;                  // SRC_FIC / SRC_MSC: src holds RING8 bytes (v + 127), not int16
-    // SRC_MSC / SRC_FIC: inverse depuncturing tables, Profile::frag uint16 mother-code
-    // positions per profile at Profile::inv_off (make_inv); null: step-major loader
-    const uint16_t *inv;
+    // SRC_MSC / SRC_FIC: inverse depuncturing tables, Profile::frag bytes per profile at
+    // Profile::inv_off (make_inv): each input's mother-code position within its 60-step
+    // tile (q mod VIT_TILE_POS); null: step-major loader
+    const uint8_t *inv;
 };
 
 // DAB+ superframe layer (k_dabplus.hip)

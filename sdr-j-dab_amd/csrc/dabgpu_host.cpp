@@ -270,11 +270,13 @@ Profile fic_profile() {                      // fic-handler.cpp:254-288
     return p;
 }
 
-// Inverse depuncturing table of a profile: the mother-code position (4 * step + e) of
+// Inverse depuncturing table of a profile: the mother-code position q = 4 * step + e of
 // each punctured input, in input order (the same rule as the kernels' idx4 /
-// in_index: PI masks per 128-bit block, then the 24-bit PI_X tail, deconvolve.cpp:172-237)
-std::vector<uint16_t> make_inv(const Profile &P) {
-    std::vector<uint16_t> inv;
+// in_index: PI masks per 128-bit block, then the 24-bit PI_X tail, deconvolve.cpp:172-237),
+// stored as its position within the ACS tile holding it (q mod VIT_TILE_POS < 240: one
+// byte, and the tile loader scatters with no offset arithmetic)
+std::vector<uint8_t> make_inv(const Profile &P) {
+    std::vector<uint8_t> inv;
     inv.reserve(P.frag);
     const int last_end = P.nseg ? P.blk_end[P.nseg - 1] : 0;
     for (int q = 0; q < 4 * (P.nbits + 6); q++) {
@@ -288,7 +290,7 @@ std::vector<uint16_t> make_inv(const Profile &P) {
             const int b = q - 128 * last_end;
             keep = b < 24 && ((P.tail_mask >> b) & 1u);
         }
-        if (keep) inv.push_back((uint16_t)q);
+        if (keep) inv.push_back((uint8_t)(q % VIT_TILE_POS));
     }
     return inv;
 }
@@ -307,7 +309,7 @@ struct dabgpu_ctx {
     int16_t *carrier_bin = nullptr;
     float *refarg = nullptr;
     uint8_t *dptab = nullptr;    // DAB+ tables (HostTables::dptab)
-    uint16_t *fic_inv = nullptr; // the FIC profile's inverse depuncturing table (make_inv)
+    uint8_t *fic_inv = nullptr;  // the FIC profile's inverse depuncturing table (make_inv)
     int32_t *err = nullptr;      // device error word (KERR_* bits)
     int32_t *h_err = nullptr;    // its pinned host copy (read after every synchronising pass)
     OfdmTables T{};
@@ -852,7 +854,7 @@ struct dabgpu_pipe {
     bool back_rec[2] = {false, false};
     int64_t run_idx = 0;
     Profile *ficprof_d = nullptr;
-    uint16_t *inv_d = nullptr;       // the subchannel profiles' inverse depuncturing tables
+    uint8_t *inv_d = nullptr;        // the subchannel profiles' inverse depuncturing tables
     // the iqBuffer feed (dabgpu_pipe_set_display): symbol 2's display carriers per ring slot
     float2 *disp_d = nullptr;        // [S][R][K]
     bool display = false;
@@ -975,10 +977,10 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
         ss[i] = p->sub[i].startAddr * 64;
         p->max_nbits = std::max(p->max_nbits, profs[i].nbits);
     }
-    std::vector<uint16_t> inv;
+    std::vector<uint8_t> inv;
     for (int i = 0; i < p->NSUB; i++) {
         profs[i].inv_off = (int32_t)inv.size();
-        const std::vector<uint16_t> v = make_inv(profs[i]);
+        const std::vector<uint8_t> v = make_inv(profs[i]);
         inv.insert(inv.end(), v.begin(), v.end());
     }
     if (inv.empty()) inv.push_back(0);
@@ -1020,7 +1022,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->dec_d[0], p->dec_sz);
     A((void **)&p->dec_d[1], p->dec_sz);
     A((void **)&p->ficprof_d, sizeof(Profile));
-    A((void **)&p->inv_d, sizeof(uint16_t) * inv.size());
+    A((void **)&p->inv_d, inv.size());
     int prio_least = 0, prio_greatest = 0;
     if (!rc && hipDeviceGetStreamPriorityRange(&prio_least, &prio_greatest) != hipSuccess) rc = fail(DABGPU_E_HIP, "priority range");
     if (!rc && (hipStreamCreateWithPriority(&p->vs[0], hipStreamNonBlocking, prio_least) != hipSuccess ||
@@ -1068,7 +1070,7 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     if (!rc) {
         if (hipMemcpy(p->prof_d, profs.data(), sizeof(Profile) * profs.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemcpy(p->substart_d, ss.data(), sizeof(int32_t) * ss.size(), hipMemcpyHostToDevice) != hipSuccess ||
-            hipMemcpy(p->inv_d, inv.data(), sizeof(uint16_t) * inv.size(), hipMemcpyHostToDevice) != hipSuccess ||
+            hipMemcpy(p->inv_d, inv.data(), inv.size(), hipMemcpyHostToDevice) != hipSuccess ||
             hipMemset(p->ring, RING8_BIAS, (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
             rc = fail(DABGPU_E_HIP, "pipe init copy failed");
     }

@@ -528,7 +528,8 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
     const int frag = __builtin_amdgcn_readfirstlane(J.prof[prof].frag);
     const int ioff = __builtin_amdgcn_readfirstlane(J.prof[prof].inv_off);
     const __amdgpu_buffer_rsrc_t rinv =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, 2 * frag, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(J.inv + ioff), (short)0, frag, 0x00020000);
+    static_assert(4 * VT == VIT_TILE_POS, "inverse tables: positions within a tile");
     u16x2 vab[IN_K];                       // the pair's inputs, packed
     uint32_t vm[IN_K];                     // their mother-code positions
     int I0 = 0, I1 = 0;
@@ -540,7 +541,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         if constexpr (KIND == SRC_MSC) ro = ro2[i & 15];
         else ro = make_int2(c[0].valid ? 0 : RO_EMPTY, c[1].valid ? 0 : RO_EMPTY);
         constexpr int ESZ = B8 ? 1 : 2;
-        const int oa = ro.x + ESZ * i, ob = ro.y + ESZ * i, oi = 2 * i;
+        const int oa = ro.x + ESZ * i, ob = ro.y + ESZ * i, oi = i;
 #pragma unroll
         for (int k = 0; k < IN_K; k++) {
             if (64 * k < I1 - I0) {
@@ -551,7 +552,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
                     vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
                     vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);
                 }
-                vm[k] = __builtin_amdgcn_raw_buffer_load_b16(rinv, oi, 128 * k, 0);
+                vm[k] = __builtin_amdgcn_raw_buffer_load_b8(rinv, oi, 64 * k, 0);
             }
         }
     };
@@ -564,7 +565,7 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         const int n = I1 - I0;
 #pragma unroll
         for (int k = 0; k < IN_K; k++) {
-            if (64 * k < n && lane + 64 * k < n) bm[vm[k] - 4 * t0] = as_u32(vab[k]);
+            if (64 * k < n && lane + 64 * k < n) bm[vm[k]] = as_u32(vab[k]);    // position in the tile
         }
         wave_sync();
         u16x2 sv[4];
