@@ -321,6 +321,133 @@ __global__ __launch_bounds__(64) void k_dp_fire(DpJob J) {
     }
 }
 
+// processSuperframe (mp4processor.cpp:146-292) of the candidate window ending at CIF cl of
+// (stream, DAB+ subchannel) sd, by one wave: RS(120,110) over the RSDims columns, the AU
+// table and AU CRCs; the verdict to J.code, the record and corrected bytes to their slots.
+// LDS: sfb [120 * DP_MAX_RS], syn_s [10 * DP_MAX_RS], rl [64 * 40], red [64] of the wave.
+__device__ void sf_decode(const DpJob &J, const GfTabs &g, int sd, int cl, uint8_t *sfb, uint32_t *syn_s,
+                          uint8_t *rl, int32_t *red, int lane) {
+    const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
+    const int br = J.dp_br[dp], sub = J.dp_sub[dp];
+    const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
+    uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
+    const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
+    window_to_lds(J, carry, stream, sub, nbytes, cl, fsz, sfb, lane);
+    for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;
+    wave_sync();
+    // syndromes S_i = sum_m r_m alpha^(i (119-m)) per column: the Horner sums of
+    // reed-solomon.cpp:231-266 (roots alpha^0..alpha^9, the 135 zero pad bytes
+    // contribute nothing).  Lane -> column lane % RS, rows lane / RS + k * (64 / RS).
+    const int per = 64 / RS;
+    if (lane < per * RS) {
+        const int j = lane % RS;
+        uint32_t acc[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) acc[i] = 0;
+        for (int m = lane / RS; m < 120; m += per) {
+            const int r = sfb[j + m * RS];
+            if (r) {
+                const int t = 119 - m;
+                int e = g.log[r];
+                acc[0] ^= g.exp[e];
+#pragma unroll
+                for (int i = 1; i < 10; i++) {
+                    e += t;
+                    if (e >= RS_NN) e -= RS_NN;
+                    acc[i] ^= g.exp[e];
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 10; i++)
+            if (acc[i]) atomicXor(&syn_s[10 * j + i], acc[i]);
+    }
+    wave_sync();
+    int ler = 0;
+    if (lane < RS) {                                     // one column per lane
+        int sy[10];
+#pragma unroll
+        for (int i = 0; i < 10; i++) sy[i] = (int)syn_s[10 * lane + i];
+        uint8_t *w = rl + lane * 40;
+        int nf = 0;
+        ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
+        for (int f = 0; f < nf; f++) {
+            const int m = w[20 + f] - RS_PAD;
+            if (m >= 0 && m < 110) sfb[lane + m * RS] ^= w[30 + f];
+        }
+    }
+    red[lane] = ler;
+    wave_sync();
+    // the reference stops at the first failing column
+    int nerr = 0, fail = 0;
+    for (int j = 0; j < RS && !fail; j++) {
+        const int l = red[j];
+        if (l > 0) nerr += l;
+        if (l < 0) fail = 1;
+    }
+    dabgpu_superframe info;
+    info.status = 2;
+    info.num_aus = 0;
+    info.n_corrected = (int16_t)nerr;
+    for (int i = 0; i < 7; i++) info.au_start[i] = 0;
+    info.au_crc_ok = 0;
+    info.reserved = 0;
+    bool ok = !fail;
+    if (ok) {
+        // AU table (:181-233)
+        const int dac = (sfb[2] >> 6) & 1, sbr = (sfb[2] >> 5) & 1;
+        int n, a[7];
+        switch (2 * dac + sbr) {
+        default:
+        case 0: n = 4; a[0] = 8; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4); a[4] = end; break;
+        case 1: n = 2; a[0] = 5; a[1] = sfb[3] * 16 + (sfb[4] >> 4); a[2] = end; break;
+        case 2: n = 6; a[0] = 11; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4);
+            a[4] = (sfb[7] & 0xf) * 256 + sfb[8]; a[5] = sfb[9] * 16 + (sfb[10] >> 4); a[6] = end; break;
+        case 3: n = 3; a[0] = 6; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
+            a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = end; break;
+        }
+        info.num_aus = (int8_t)n;
+        for (int i = 0; i < 7; i++) info.au_start[i] = (int16_t)(i <= n ? a[i] : 0);
+        int bad = n;                                     // first AU with an impossible layout
+        for (int i = 0; i < n; i++) {
+            const int len = a[i + 1] - a[i] - 2;
+            if (a[i + 1] < a[i] || len >= 960 || len < 0) { bad = i; break; }
+        }
+        // dabPlus_crc (mp4processor.cpp:40-61) of AU i over [a[i], a[i+1]): lane l
+        // runs the table CRC over its slice (lane 0 from the 0xFFFF preset, the others
+        // from 0), shifts it past the bytes after the slice, and the slices XOR
+        // together.  Bytes past the superframe read as zero.
+        uint32_t mask = 0;
+        for (int i = 0; i < bad; i++) {
+            const int ai = a[i], len = a[i + 1] - ai - 2, limit = end - ai;
+            const int cs = (len + 63) >> 6;
+            const int k0 = min(len, lane * cs), k1 = min(len, k0 + cs);
+            uint32_t acc = lane == 0 ? 0xFFFFu : 0u;
+            for (int k = k0; k < k1; k++) {
+                const uint32_t b = k < limit ? sfb[ai + k] : 0u;
+                acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ b) & 0xFFu]) & 0xFFFFu;
+            }
+            if (acc) acc = crc_mulmod(acc, g.pow8[len - k1]);
+            acc = wave_xor(acc);
+            const uint32_t hi = len < limit ? sfb[ai + len] : 0u, lo = len + 1 < limit ? sfb[ai + len + 1] : 0u;
+            if (((~((hi << 8) | lo) & 0xFFFFu) ^ acc) == 0) mask |= 1u << i;
+        }
+        info.au_crc_ok = (uint8_t)(mask & 0x3F);
+        ok = bad == n;
+    }
+    if (ok) {
+        info.status = 3;
+        uint8_t *o = J.sf_out + (((int64_t)stream * J.ncif + cl) * J.ndp + dp) * J.sf_stride;
+        for (int i = lane; i < end; i += 64) o[i] = sfb[i];
+    }
+    if (lane == 0) {
+        J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
+        *code = (uint8_t)info.status;
+    }
+}
+
 __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     __shared__ GfTabs g;
     __shared__ __attribute__((aligned(16))) uint8_t sfb[120 * DP_MAX_RS];
@@ -334,126 +461,7 @@ __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
     for (int ci = blockIdx.x; ci < ncand; ci += gridDim.x) {
         wave_sync();                                         // the previous candidate's LDS reads are done
         const int id = J.cand[ci];
-        const int cl = id % J.ncif, sd = id / J.ncif;
-        const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
-        const int br = J.dp_br[dp], sub = J.dp_sub[dp];
-        const int RS = br / 8, nbytes = 3 * br, fsz = 120 * RS, end = 110 * RS;
-        uint8_t *code = J.code + (int64_t)sd * J.ncif + cl;
-        const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
-        window_to_lds(J, carry, stream, sub, nbytes, cl, fsz, sfb, lane);
-        for (int p = lane; p < 10 * RS; p += 64) syn_s[p] = 0;
-        wave_sync();
-        // syndromes S_i = sum_m r_m alpha^(i (119-m)) per column: the Horner sums of
-        // reed-solomon.cpp:231-266 (roots alpha^0..alpha^9, the 135 zero pad bytes
-        // contribute nothing).  Lane -> column lane % RS, rows lane / RS + k * (64 / RS).
-        const int per = 64 / RS;
-        if (lane < per * RS) {
-            const int j = lane % RS;
-            uint32_t acc[10];
-    #pragma unroll
-            for (int i = 0; i < 10; i++) acc[i] = 0;
-            for (int m = lane / RS; m < 120; m += per) {
-                const int r = sfb[j + m * RS];
-                if (r) {
-                    const int t = 119 - m;
-                    int e = g.log[r];
-                    acc[0] ^= g.exp[e];
-    #pragma unroll
-                    for (int i = 1; i < 10; i++) {
-                        e += t;
-                        if (e >= RS_NN) e -= RS_NN;
-                        acc[i] ^= g.exp[e];
-                    }
-                }
-            }
-    #pragma unroll
-            for (int i = 0; i < 10; i++)
-                if (acc[i]) atomicXor(&syn_s[10 * j + i], acc[i]);
-        }
-        wave_sync();
-        int ler = 0;
-        if (lane < RS) {                                     // one column per lane
-            int sy[10];
-    #pragma unroll
-            for (int i = 0; i < 10; i++) sy[i] = (int)syn_s[10 * lane + i];
-            uint8_t *w = rl + lane * 40;
-            int nf = 0;
-            ler = rs_solve(sy, g, w, w + 10, w + 20, w + 30, &nf);
-            for (int f = 0; f < nf; f++) {
-                const int m = w[20 + f] - RS_PAD;
-                if (m >= 0 && m < 110) sfb[lane + m * RS] ^= w[30 + f];
-            }
-        }
-        red[lane] = ler;
-        wave_sync();
-        // the reference stops at the first failing column
-        int nerr = 0, fail = 0;
-        for (int j = 0; j < RS && !fail; j++) {
-            const int l = red[j];
-            if (l > 0) nerr += l;
-            if (l < 0) fail = 1;
-        }
-        dabgpu_superframe info;
-        info.status = 2;
-        info.num_aus = 0;
-        info.n_corrected = (int16_t)nerr;
-        for (int i = 0; i < 7; i++) info.au_start[i] = 0;
-        info.au_crc_ok = 0;
-        info.reserved = 0;
-        bool ok = !fail;
-        if (ok) {
-            // AU table (:181-233)
-            const int dac = (sfb[2] >> 6) & 1, sbr = (sfb[2] >> 5) & 1;
-            int n, a[7];
-            switch (2 * dac + sbr) {
-            default:
-            case 0: n = 4; a[0] = 8; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
-                a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4); a[4] = end; break;
-            case 1: n = 2; a[0] = 5; a[1] = sfb[3] * 16 + (sfb[4] >> 4); a[2] = end; break;
-            case 2: n = 6; a[0] = 11; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
-                a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = sfb[6] * 16 + (sfb[7] >> 4);
-                a[4] = (sfb[7] & 0xf) * 256 + sfb[8]; a[5] = sfb[9] * 16 + (sfb[10] >> 4); a[6] = end; break;
-            case 3: n = 3; a[0] = 6; a[1] = sfb[3] * 16 + (sfb[4] >> 4);
-                a[2] = (sfb[4] & 0xf) * 256 + sfb[5]; a[3] = end; break;
-            }
-            info.num_aus = (int8_t)n;
-            for (int i = 0; i < 7; i++) info.au_start[i] = (int16_t)(i <= n ? a[i] : 0);
-            int bad = n;                                     // first AU with an impossible layout
-            for (int i = 0; i < n; i++) {
-                const int len = a[i + 1] - a[i] - 2;
-                if (a[i + 1] < a[i] || len >= 960 || len < 0) { bad = i; break; }
-            }
-            // dabPlus_crc (mp4processor.cpp:40-61) of AU i over [a[i], a[i+1]): lane l
-            // runs the table CRC over its slice (lane 0 from the 0xFFFF preset, the others
-            // from 0), shifts it past the bytes after the slice, and the slices XOR
-            // together.  Bytes past the superframe read as zero.
-            uint32_t mask = 0;
-            for (int i = 0; i < bad; i++) {
-                const int ai = a[i], len = a[i + 1] - ai - 2, limit = end - ai;
-                const int cs = (len + 63) >> 6;
-                const int k0 = min(len, lane * cs), k1 = min(len, k0 + cs);
-                uint32_t acc = lane == 0 ? 0xFFFFu : 0u;
-                for (int k = k0; k < k1; k++) {
-                    const uint32_t b = k < limit ? sfb[ai + k] : 0u;
-                    acc = ((acc << 8) ^ g.crc[((acc >> 8) ^ b) & 0xFFu]) & 0xFFFFu;
-                }
-                if (acc) acc = crc_mulmod(acc, g.pow8[len - k1]);
-                acc = wave_xor(acc);
-                const uint32_t hi = len < limit ? sfb[ai + len] : 0u, lo = len + 1 < limit ? sfb[ai + len + 1] : 0u;
-                if (((~((hi << 8) | lo) & 0xFFFFu) ^ acc) == 0) mask |= 1u << i;
-            }
-            info.au_crc_ok = (uint8_t)(mask & 0x3F);
-            ok = bad == n;
-        }
-        if (ok) {
-            info.status = 3;
-            uint8_t *o = J.sf_out + (((int64_t)stream * J.ncif + cl) * J.ndp + dp) * J.sf_stride;
-            for (int i = lane; i < end; i += 64) o[i] = sfb[i];
-        }
-        if (lane == 0) {
-            J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] = info;
-            *code = (uint8_t)info.status;
-        }
+        sf_decode(J, g, id / J.ncif, id % J.ncif, sfb, syn_s, rl, red, lane);
     }
 }
 
@@ -462,8 +470,9 @@ __global__ __launch_bounds__(64) void k_dp_superframe(DpJob J) {
 // candidates are evaluated; their verdicts come from k_dp_superframe.  Writes the
 // records of the CIFs without an evaluated superframe, the state, and the carry
 // (the run's last 4 CIFs as bytes) for the next run.
-__global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
-    const int lane = threadIdx.x, sd = blockIdx.x;
+// addtoFrame's block counting (mp4processor.cpp:107-145) over the run's CIFs of sd, by one
+// wave, and the carry (the run's last 4 CIFs) for the next run; nc: LDS [4 * 3 * 384]
+__device__ void dp_walk(const DpJob &J, int sd, uint8_t *nc, int lane) {
     const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
     const int br = J.dp_br[dp], sub = J.dp_sub[dp], nbytes = 3 * br;
     DpState st = J.state[sd];
@@ -504,7 +513,6 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
     }
     // carry = the stream's last 4 delivered CIFs (oldest first); with fewer than 4 new
     // ones the older part comes from the previous carry (staged: it is overwritten)
-    __shared__ uint8_t nc[4 * 3 * 384];
     uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
     for (int p0 = 0; p0 < 4 * nbytes; p0 += 8 * 64) {    // a lane's loads in flight together
         uint32_t v[8];
@@ -527,9 +535,64 @@ __global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
     if (lane == 0) J.state[sd] = st;
 }
 
+__global__ __launch_bounds__(64) void k_dp_walk(DpJob J) {
+    __shared__ uint8_t nc[4 * 3 * 384];
+    dp_walk(J, blockIdx.x, nc, threadIdx.x);
+}
+
+// The whole layer for one (stream, DAB+ subchannel) in one workgroup of DP_WAVES waves: the
+// fire code of every CIF window (one thread per CIF), the passing candidates' superframes
+// (the waves take them in turn), then the walk -- one launch instead of a queue reset and
+// three dependent launches, the GF tables loaded once per workgroup.  The workgroup's own
+// verdicts are all the walk reads, so no grid-wide step.
+constexpr int DP_WAVES = 8;
+__global__ __launch_bounds__(64 * DP_WAVES) void k_dp_layer(DpJob J) {
+    __shared__ __attribute__((aligned(16))) GfTabs g;
+    __shared__ __attribute__((aligned(16))) uint8_t sfb[DP_WAVES][120 * DP_MAX_RS];
+    __shared__ uint32_t syn_s[DP_WAVES][10 * DP_MAX_RS];
+    __shared__ uint8_t rl[DP_WAVES][64 * 40];
+    __shared__ int32_t red[DP_WAVES][64];
+    __shared__ int16_t cand[4 * 512];
+    __shared__ int32_t ncand;
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6, sd = blockIdx.x;
+    const int stream = sd / J.ndp, dp = sd - stream * J.ndp;
+    const int br = J.dp_br[dp], sub = J.dp_sub[dp], nbytes = 3 * br;
+    const uint32_t *tabs32 = (const uint32_t *)J.tabs;
+    for (int i = t; i < (int)sizeof(GfTabs) / 4; i += 64 * DP_WAVES) ((uint32_t *)&g)[i] = tabs32[i];
+    if (t == 0) ncand = 0;
+    __syncthreads();
+    const uint8_t *carry = J.ring + (int64_t)sd * (120 * DP_MAX_RS);
+    for (int cl = t; cl < J.ncif; cl += 64 * DP_WAVES) {
+        // a window holding an undelivered CIF (de-interleaver warm-up, or a CIF slot the
+        // stream did not fill in this run) is never evaluated
+        bool ok = !(cl >= J.ncifs[stream] || J.cif0s[stream] + cl - 4 < 16);
+        if (ok) {
+            uint32_t x[11];
+#pragma unroll
+            for (int p = 0; p < 11; p++) x[p] = window_byte(J, carry, stream, sub, nbytes, cl, p);
+            ok = fire_ok(x, g.fire);
+        }
+        J.code[(int64_t)sd * J.ncif + cl] = ok ? 1 : 0;
+        if (ok) cand[atomicAdd(&ncand, 1)] = (int16_t)cl;
+    }
+    __syncthreads();
+    const int nc = ncand;
+    for (int ci = w; ci < nc; ci += DP_WAVES) {
+        sf_decode(J, g, sd, cand[ci], sfb[w], syn_s[w], rl[w], red[w], lane);
+        wave_sync();                                     // this wave's LDS reads are done
+    }
+    __syncthreads();                                     // every verdict of sd written (J.code)
+    if (w == 0) dp_walk(J, sd, sfb[1], lane);            // (the carry staging reuses an idle stage)
+}
+
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job) {
     if (job.ndp <= 0 || job.nstreams <= 0) return hipSuccess;
     if (job.ncif < 4) return hipErrorInvalidValue;       // the carry holds the last 4 CIFs
+    static const bool split = [] { const char *e = getenv("DABGPU_DP_SPLIT"); return e && e[0] == '1'; }();   // A/B
+    if (!split && job.ncif <= 4 * 512) {
+        hipLaunchKernelGGL(k_dp_layer, dim3(job.nstreams * job.ndp), dim3(64 * DP_WAVES), 0, st, job);
+        return hipGetLastError();
+    }
     hipError_t e = hipMemsetAsync(job.ncand, 0, sizeof(int32_t), st);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_dp_fire, dim3(job.nstreams * job.ndp), dim3(64), 0, st, job);
