@@ -665,7 +665,7 @@ def main():
         "metric": "DAB Mode-I symbols/sec (and real-time ensembles/GPU) at 1/2/4/8 MI355X",
         "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f32 (OFDM) + u16x2 packed path metrics (Viterbi, exact)",
+        "vs_baseline": None, "dtype": "f32 (OFDM) + u8 soft bits (ring) + u16x2 packed path metrics (Viterbi, exact)",
         "data": f"synthetic (dabsynth transmitter, 30 dB SNR, CFO {args.cfo:g} Hz)"
                 + (", int16 .sdr samples scattered from rank 0 over RCCL" if rccl else ""),
         "config": {"workload": wl_desc, "ensembles_per_gpu": E, "frames_per_step": F,
