@@ -80,7 +80,7 @@ typedef struct {
     int16_t n_corrected;    /* RS symbols corrected (sum over the RSDims codewords) */
     int16_t au_start[7];    /* au_start[0..num_aus] */
     uint8_t au_crc_ok;      /* bit i: AU i passed dabPlus_crc */
-    uint8_t reserved;
+    uint8_t reserved;       /* compact output: the superframe's slot (0xFF: none); else 0 */
 } dabgpu_superframe;
 
 /* Per-frame front-end parameters (ofdm-processor.cpp:344-446), one per
@@ -325,6 +325,14 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, co
  *              corrected superframe bytes where info.status == 3
  *   info_d     [n_streams][4*n_frames][n_dabplus] */
 int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes_d, int32_t sf_stride, dabgpu_superframe *info_d);
+/* Compact superframe bytes for the following dabgpu_pipe_dabplus calls (on = 1): only the
+ * superframes that complete in the run are stored, per (stream, DAB+ subchannel) in CIF
+ * order -- sf_bytes_d [n_streams][n_dabplus][DABGPU_SF_SLOTS(n_frames)][sf_stride], the
+ * k-th at slot k, and its info record's `reserved` byte is k (0xFF for records without
+ * bytes).  One CIF in five carries a superframe, so this is the form to copy to the host
+ * (dabgpu_pipe_fetch).  At most 512 frames per run. */
+#define DABGPU_SF_SLOTS(n_frames) ((4 * (n_frames) + 4) / 5 + 1)
+int dabgpu_pipe_set_dabplus_compact(dabgpu_pipe *p, int on);
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
 /* [n_streams][n_frames] records of the last dabgpu_pipe_run */
 int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info_h);

@@ -163,6 +163,11 @@ struct DpJob {
     const uint8_t *tabs;            // DP_TAB_BYTES: GF exp, log, fire table, alpha^i multiply, CRC
     int32_t *cand;                  // [S * ndp * ncif] queue of fire-code-passing candidates
     int32_t *ncand;                 // its length (reset per launch)
+    // compact output (dabgpu_pipe_set_dabplus_compact): the superframes that complete in
+    // the run, per (stream, DAB+ subchannel) in CIF order, at sf_compact[(s*ndp+dp)*kmax+k]
+    // (stride sf_stride); sf_out is then the pipeline's own sparse scratch
+    uint8_t *sf_compact;
+    int32_t kmax;
 };
 
 hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,

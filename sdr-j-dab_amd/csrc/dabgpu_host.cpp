@@ -833,6 +833,11 @@ struct dabgpu_pipe {
     std::vector<dabgpu_frame_info> last_info;   // [S][F] observables of the last run
     // DAB+ superframe layer (mp4Processor per DAB+ subchannel and stream)
     int NDP = 0, dp_max_rs = 0;
+    // compact superframe output (dabgpu_pipe_set_dabplus_compact): the layer decodes into
+    // this sparse scratch and stores the run's superframes in CIF order for the caller
+    bool dp_compact = false;
+    uint8_t *sf_sparse_d = nullptr;
+    size_t sf_sparse_bytes = 0;
     int32_t *dp_sub_d = nullptr;
     int16_t *dp_br_d = nullptr;
     uint8_t *dp_ring_d = nullptr;     // [S][NDP][120*DP_MAX_RS]
@@ -1103,6 +1108,7 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_cif0,
                     (void *)p->h_ncif, (void *)p->h_slots, (void *)p->h_berr})
         if (h) (void)hipHostFree(h);
+    if (p->sf_sparse_d) (void)hipFree(p->sf_sparse_d);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->inv_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
                     (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
                     (void *)p->cif0_d, (void *)p->ncif_d, (void *)p->berr_d,
@@ -1781,6 +1787,21 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.cand = p->dp_cand_d + 1;
     J.sf_out = sf_bytes;
     J.sf_stride = sf_stride;
+    if (p->dp_compact) {
+        const size_t need = (size_t)p->S * 4 * p->F * p->NDP * (size_t)sf_stride;
+        if (need > p->sf_sparse_bytes) {             // (stream-ordered: earlier layers are done with it)
+            HIPCHK(hipDeviceSynchronize());
+            if (p->sf_sparse_d) HIPCHK(hipFree(p->sf_sparse_d));
+            p->sf_sparse_d = nullptr;
+            p->sf_sparse_bytes = 0;
+            HIPCHK(hipMalloc((void **)&p->sf_sparse_d, need));
+            p->sf_sparse_bytes = need;
+        }
+        J.sf_out = p->sf_sparse_d;
+        J.sf_compact = sf_bytes;
+        J.kmax = DABGPU_SF_SLOTS(p->F);
+        if (4 * p->F > 4 * 512) return fail(DABGPU_E_UNSUP, "compact DAB+ output: at most 512 frames per run");
+    }
     J.info = info;
     J.tabs = c->dptab;
     // on the last run's back-end stream (after its MSC), after the previous
@@ -1892,6 +1913,11 @@ int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot) {
 int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on) {
     if (!p) return fail(DABGPU_E_ARG, "bad args");
     p->packed = on != 0;
+    return 0;
+}
+int dabgpu_pipe_set_dabplus_compact(dabgpu_pipe *p, int on) {
+    if (!p) return fail(DABGPU_E_ARG, "bad args");
+    p->dp_compact = on != 0;
     return 0;
 }
 int dabgpu_pipe_fetch(dabgpu_pipe *p, void *dst_h, const void *src_d, size_t bytes) {

@@ -583,13 +583,44 @@ __global__ __launch_bounds__(64 * DP_WAVES) void k_dp_layer(DpJob J) {
     }
     __syncthreads();                                     // every verdict of sd written (J.code)
     if (w == 0) dp_walk(J, sd, sfb[1], lane);            // (the carry staging reuses an idle stage)
+    if (!J.sf_compact) return;
+    // compact output: the run's decoded superframes of sd in CIF order (after the walk,
+    // status 3 marks exactly the ones the reference evaluated and decoded), slot k of the
+    // k-th; the record's `reserved` byte carries k (0xFF: not stored)
+    __syncthreads();                                     // the walk's records are written
+    if (w == 0) {
+        int k = 0;
+        for (int c0 = 0; c0 < J.ncif; c0 += 64) {
+            const int cl = c0 + lane;
+            dabgpu_superframe *r = cl < J.ncif ? &J.info[((int64_t)stream * J.ncif + cl) * J.ndp + dp] : nullptr;
+            const bool dec = r && r->status == 3;
+            const uint64_t bal = __ballot(dec);
+            const int kk = k + __popcll(bal & ((1ull << lane) - 1ull));
+            if (dec) {
+                r->reserved = (uint8_t)(kk < J.kmax ? kk : 0xFF);
+                if (kk < J.kmax) cand[kk] = (int16_t)cl;
+            } else if (r) {
+                r->reserved = 0xFF;
+            }
+            k += __popcll(bal);
+        }
+        if (lane == 0) ncand = k < J.kmax ? k : J.kmax;
+    }
+    __syncthreads();
+    const int nk = ncand, end = 110 * (br / 8);
+    for (int q = w; q < nk; q += DP_WAVES) {             // a wave per superframe, a byte per lane
+        const uint8_t *src = J.sf_out + (((int64_t)stream * J.ncif + cand[q]) * J.ndp + dp) * J.sf_stride;
+        uint8_t *dst = J.sf_compact + ((int64_t)sd * J.kmax + q) * J.sf_stride;
+        for (int i = lane; i < end; i += 64) dst[i] = src[i];
+    }
 }
 
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job) {
     if (job.ndp <= 0 || job.nstreams <= 0) return hipSuccess;
     if (job.ncif < 4) return hipErrorInvalidValue;       // the carry holds the last 4 CIFs
     static const bool split = [] { const char *e = getenv("DABGPU_DP_SPLIT"); return e && e[0] == '1'; }();   // A/B
-    if (!split && job.ncif <= 4 * 512) {
+    if (job.sf_compact && job.ncif > 4 * 512) return hipErrorInvalidValue;   // the fused layer only
+    if (job.sf_compact || (!split && job.ncif <= 4 * 512)) {
         hipLaunchKernelGGL(k_dp_layer, dim3(job.nstreams * job.ndp), dim3(64 * DP_WAVES), 0, st, job);
         return hipGetLastError();
     }

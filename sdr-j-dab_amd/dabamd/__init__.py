@@ -121,6 +121,7 @@ def lib() -> C.CDLL:
             "dabgpu_pipe_frame_info": ([vp, vp], i32),
             "dabgpu_pipe_control": ([vp, i32, i32], i32),
             "dabgpu_pipe_softbits": ([vp, C.POINTER(vp), C.POINTER(C.c_int32)], i32),
+            "dabgpu_pipe_set_dabplus_compact": ([vp, i32], i32),
             "dabgpu_pipe_frame_slot": ([vp, i32, C.POINTER(C.c_int32)], i32),
             "dabgpu_pipe_frames": ([vp, vp, vp], i32),
             "dabgpu_pipe_set_display": ([vp, i32], i32),
@@ -562,9 +563,21 @@ class Pipeline:
         msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), ms)) if self.subch else None
         return fic, crc, msc, valid
 
+    def set_dabplus_compact(self, on: bool = True) -> None:
+        """compact superframe bytes (dabgpu_pipe_set_dabplus_compact): dabplus() then returns
+        bytes [S, n_dabplus, sf_slots, sf_stride], the run's superframes in CIF order, and
+        each record's `reserved` is its slot"""
+        _chk(lib().dabgpu_pipe_set_dabplus_compact(self.h, int(on)), "dabgpu_pipe_set_dabplus_compact")
+        self.dp_compact = bool(on)
+
+    @property
+    def sf_slots(self) -> int:
+        return (4 * self.F + 4) // 5 + 1                  # DABGPU_SF_SLOTS
+
     def dabplus(self, download: bool = True):
         """DAB+ superframe layer over the CIFs of the last run() (mp4processor.cpp:107-292).
-        Returns (info [S, 4F, n_dabplus] Superframe records, bytes [S, 4F, n_dabplus, sf_stride])."""
+        Returns (info [S, 4F, n_dabplus] Superframe records, bytes [S, 4F, n_dabplus, sf_stride]
+        -- or [S, n_dabplus, sf_slots, sf_stride] with set_dabplus_compact)."""
         self.sf_d, self.sfi_d = self._sf[(self._run - 1) & 1]
         _chk(lib().dabgpu_pipe_dabplus(self.h, self.sf_d.ptr, self.sf_stride, self.sfi_d.ptr), "dabgpu_pipe_dabplus")
         if not download:
@@ -573,7 +586,10 @@ class Pipeline:
         nd = len(self.dp)
         raw = self.sfi_d.download(np.uint8, self.S * 4 * self.F * nd * C.sizeof(Superframe))
         info = np.frombuffer(raw.tobytes(), dtype=SUPERFRAME_DTYPE).reshape(self.S, 4 * self.F, nd)
-        sf = self.sf_d.download(np.uint8, (self.S, 4 * self.F, nd, self.sf_stride))
+        if getattr(self, "dp_compact", False):
+            sf = self.sf_d.download(np.uint8, (self.S, nd, self.sf_slots, self.sf_stride))
+        else:
+            sf = self.sf_d.download(np.uint8, (self.S, 4 * self.F, nd, self.sf_stride))
         return info, sf
 
     STAGES = ("prs_sync", "block0", "demod", "fic", "msc_acs", "msc_traceback", "dabplus")

@@ -483,3 +483,48 @@ def test_fetch_to_host_equals_download(ctx):
     finally:
         for b in hb:
             b.free()
+
+
+def test_dabplus_compact_output_equals_sparse(ctx):
+    """dabgpu_pipe_set_dabplus_compact: the run's decoded superframes in CIF order, slot k
+    of the k-th, the record's `reserved` = k -- the same bytes and records as the sparse
+    layout, over runs that carry superframes across their seams (11 dB: RS corrections)"""
+    import dabamd
+    sub = [(0, 48, 64, 0o103, 0, 1), (48, 36, 48, 0o103, 0, 1), (84, 96, 128, 3, 1, 0)]
+    F, runs = 4, 6
+    iqs = _gen(sub, F * runs + 1, [91, 92], 11.0)
+    S = len(iqs)
+    lens = [len(x) // 2 for x in iqs]
+    stride = max(lens)
+    buf = np.zeros((S, 2 * stride), np.float32)
+    for s, x in enumerate(iqs):
+        buf[s, :len(x)] = x
+    diq = ctx.put(buf)
+    subs = [dabamd.Subch(sc[0], sc[1], sc[2], sc[3], 0 if sc[4] else 1, dabamd.SUBCH_DABPLUS if sc[5] else 0)
+            for sc in sub]
+    pa, pb = dabamd.Pipeline(ctx, S, F, subs), dabamd.Pipeline(ctx, S, F, subs)
+    for p in (pa, pb):
+        p.set_packed(True)
+    pb.set_dabplus_compact(True)
+    nd, decoded = len(pa.dp), 0
+    for r in range(runs):
+        pa.run(diq, stride, lens, download=False, partial=True)
+        pb.run(diq, stride, lens, download=False, partial=True)
+        ia, ba = pa.dabplus()
+        ib, bb = pb.dabplus()
+        for name in ("status", "num_aus", "n_corrected", "au_start", "au_crc_ok"):
+            assert np.array_equal(ia[name], ib[name]), (r, name)
+        for s in range(S):
+            for d in range(nd):
+                end = 110 * (pa.dp[d].bitRate // 8)
+                k = 0
+                for c in range(4 * F):
+                    if ia["status"][s, c, d] == 3:
+                        assert ib["reserved"][s, c, d] == k, (r, s, c, d)
+                        assert np.array_equal(bb[s, d, k, :end], ba[s, c, d, :end]), (r, s, c, d)
+                        k += 1
+                        decoded += 1
+                    else:
+                        assert ib["reserved"][s, c, d] == 0xFF
+                assert k <= pb.sf_slots
+    assert decoded >= S * nd * 2
