@@ -731,8 +731,10 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
     n_fic, n_crc = E * F * 4 * 768, E * F * 12
     n_msc = E * 4 * F * ns * pipe.msc_stride_packed
     nd = len(pipe.dp)
+    if nd:                                                      # only the run's superframes travel
+        pipe.set_dabplus_compact(True)
     n_sfi = E * 4 * F * nd * 16 if nd else 0                     # dabgpu_superframe records
-    n_sf = E * 4 * F * nd * pipe.sf_stride if nd else 0
+    n_sf = E * nd * pipe.sf_slots * pipe.sf_stride if nd else 0  # compact: DABGPU_SF_SLOTS per subchannel
     total = n_fic + n_crc + n_msc + n_sfi + n_sf
     hb = [dabamd.HostBuf(ctx, total) for _ in range(2)]
     valids = [None, None]
@@ -767,12 +769,16 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
     check = check_step(truth, P, st0, st1, fic, crc, msc, valids[steps & 1], subch)
     for b in hb:
         b.free()
+    if nd:
+        pipe.sync()
+        pipe.set_dabplus_compact(False)
     world = dist.get_world_size() if dist is not None else 1
     return {"value": world * E * F * 76 * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
             "bytes_to_host_per_step": total, "pcie_GBps": total * steps / el / 1e9,
             "msc_format": "8 bits per byte, msb first (dabgpu_pipe_set_packed)",
             "checked_last_step_from_host_memory": check,
-            "note": "FIC bits + CRC flags + packed MSC bytes" + (" + DAB+ superframe records and bytes" if nd else "")
+            "note": "FIC bits + CRC flags + packed MSC bytes" + (" + DAB+ superframe records and the run's "
+                                                                 "superframe bytes (compact)" if nd else "")
                     + " of every step copied to pinned host memory behind its run's channel decoding "
                       "(dabgpu_pipe_fetch), overlapping the next run"}
 

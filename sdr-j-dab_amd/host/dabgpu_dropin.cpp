@@ -255,6 +255,8 @@ ensembleDecoder::ensembleDecoder(const config &cfg) : cfg_(cfg) {
     maxbits_ = maxbits;
     sf_stride_ = std::max(16, 110 * maxrs);
     const size_t SF = (size_t)cfg.n_streams * cfg.n_frames;
+    // only the superframes a run completes cross PCIe (DABGPU_SF_SLOTS per subchannel)
+    if (ndp_) chk(dabgpu_pipe_set_dabplus_compact(pipe_, 1), "dabgpu_pipe_set_dabplus_compact");
     fic_.resize(SF * 4 * 768);
     crc_.resize(SF * 12);
     msc_.resize(std::max<size_t>(1, SF * 4 * cfg.subch.size() * msc_stride_));
@@ -340,7 +342,8 @@ bool ensembleDecoder::step() {
         chk(dabgpu_pipe_sync(pipe_), "dabgpu_pipe_sync");
         if (sf_cb_) {
             std::vector<dabgpu_superframe> info((size_t)S * 4 * F * ndp_);
-            std::vector<uint8_t> bytes(info.size() * sf_stride_);
+            const int slots = DABGPU_SF_SLOTS(F);
+            std::vector<uint8_t> bytes((size_t)S * ndp_ * slots * sf_stride_);
             sfi_.download(info.data(), info.size() * sizeof(dabgpu_superframe));
             sf_.download(bytes.data(), bytes.size());
             for (size_t r = 0; r < info.size(); r++) {
@@ -349,8 +352,11 @@ bool ensembleDecoder::step() {
                 const int c = (int)((r / ndp_) % (4 * F));
                 const int s = (int)(r / ndp_ / (4 * F));
                 const int k = dp_index_[d];
-                sf_cb_(s, 4 * frames_done_[s] + c, k, info[r], bytes.data() + r * sf_stride_,
-                    info[r].status == 3 ? 110 * (cfg_.subch[k].bitRate / 8) : 0);
+                const int slot = info[r].reserved;           // compact output: the superframe's slot
+                const bool has = info[r].status == 3 && slot < slots;
+                sf_cb_(s, 4 * frames_done_[s] + c, k, info[r],
+                       bytes.data() + (((size_t)s * ndp_ + d) * slots + (has ? slot : 0)) * sf_stride_,
+                       has ? 110 * (cfg_.subch[k].bitRate / 8) : 0);
             }
         }
     }
