@@ -14,10 +14,10 @@ namespace dab {
 // on the search's outcome is computed by all 64 lanes: the NCO index of a sample is a
 // closed form of its position inside the attempt (phase 0 for the 20*T_s + 50 samples
 // that build sLevel, coarse+fine after), so lanes mix a block of samples and form
-// their L1 norms (jan_abs) and magnitudes (abs) in parallel.  Lane 0 then runs the
-// reference's sequential state machine over the block from LDS: the double-precision
-// sLevel IIR rounded to float at every sample, the 50-sample envelope sum and the
-// dip / end-of-dip thresholds.  A restart (goto notSynced) changes the mixing of the
+// their L1 norms (jan_abs) and magnitudes (abs) in parallel.  The reference's state
+// machine then walks the block from LDS: the double-precision sLevel IIR rounded to
+// float at every sample, the 50-sample envelope sum and the dip / end-of-dip
+// thresholds.  A restart (goto notSynced) changes the mixing of the
 // samples after it: the block is recomputed from there.
 __device__ __forceinline__ float jan_abs(float2 z) { return fabsf(z.x) + fabsf(z.y); }
 
@@ -34,41 +34,48 @@ __device__ __forceinline__ int32_t acq_lp(int64_t p, int64_t a, int32_t lpa, int
     return (int32_t)(t < 0 ? t + INPUT_RATE : t);
 }
 
-// The sequential part runs on lane 0 as one tight loop per state.  Per sample the
-// sLevel IIR needs only its own chain (cvt, mul, add, cvt: the 0.00001 * jan_abs term is
-// formed by all lanes beforehand, pj[]), the envelope sum one float add: the value
-// leaving the 50-sample window was inserted at least 43 samples earlier, so a group of 8
-// samples reads its 8 outgoing values before its own insertions.  While searching the
-// dip, a group runs both chains over its 8 samples and then the 8 threshold tests side
-// by side, keeping the states up to the first test that fails (the reference's loop
-// stops there).  The threshold tests
+// Only the two chains are sequential.  Per sample the sLevel IIR needs its own chain
+// (cvt, mul, add, cvt: the 0.00001 * jan_abs term is formed by all lanes beforehand,
+// pj[]), the envelope sum one float add of a difference the lanes formed beforehand: the
+// value leaving the 50-sample window entered 50 samples earlier, before the group or
+// inside it.  While searching, lane 0 runs both chains over a group of 64 samples, then
+// the 64 lanes test the 64 states side by side and the group keeps the states up to the
+// first test that fails (the reference's loop stops there).  The threshold tests
 // (currentStrength / 50 against 0.40 / 0.75 * sLevel, a float division compared in
 // double) take a multiply by 0.02f and fall back to the IEEE division only within 2^-21
 // of the threshold: the quotient and the product differ by less than 2^-22 of it.
 __device__ __forceinline__ bool q50_gt(float cur, double t) {     // fl(cur / 50) > t
+#pragma clang fp contract(off)
     const double qa = (double)(cur * 0.02f);
     if (fabs(qa - t) > 0x1p-21 * fabs(qa)) return qa > t;
     return (double)(cur / 50) > t;
 }
 __device__ __forceinline__ bool q50_lt(float cur, double t) {     // fl(cur / 50) < t
+#pragma clang fp contract(off)
     const double qa = (double)(cur * 0.02f);
     if (fabs(qa - t) > 0x1p-21 * fabs(qa)) return qa < t;
     return (double)(cur / 50) < t;
 }
 __device__ __forceinline__ float slevel_next(float s, double pj) {
+#pragma clang fp contract(off)                                     // two roundings, as the reference's mulsd + addsd
     return (float)(pj + (1 - 0.00001) * (double)s);                // ofdm-processor.cpp:225
 }
 
 __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, const AcqJob *__restrict__ jobs, int n,
                                                 const float2 *__restrict__ osc, AcqResult *__restrict__ res) {
 #pragma clang fp contract(off)
-    __shared__ __attribute__((aligned(16))) float ja[ACQ_BLK + 8];
-    __shared__ __attribute__((aligned(16))) float hy[ACQ_BLK + 8];
-    __shared__ __attribute__((aligned(16))) double pj[ACQ_BLK + 8];
-    __shared__ float env[64];
-    __shared__ int32_t ev[2];                        // lane 0 -> wave: event kind, sample index in block
+    // a group reads up to 64 samples past its start: the arrays carry 64 zeros behind the block
+    __shared__ __attribute__((aligned(16))) float ja[ACQ_BLK + 64];
+    __shared__ __attribute__((aligned(16))) float hy[ACQ_BLK + 64];
+    __shared__ __attribute__((aligned(16))) double pj[ACQ_BLK + 64];
+    __shared__ float env[64];                        // the 50-sample envelope window (ring of 64)
+    __shared__ __attribute__((aligned(16))) float dd[64];      // group: v_u - (value leaving at u)
+    __shared__ __attribute__((aligned(16))) float2 sc[65];     // group: (sLevel, strength) before sample u
     const int lane = threadIdx.x;
     if ((int)blockIdx.x >= n) return;
+    ja[ACQ_BLK + lane] = 0.0f;
+    hy[ACQ_BLK + lane] = 0.0f;
+    pj[ACQ_BLK + lane] = 0.0;
     // a latency-bound chain on one lane: first pick on its SIMD, so a search launched while
     // the pipeline's ACS waves fill the SIMDs (a sync loss) is not starved of issue slots
     __builtin_amdgcn_s_setprio(3);
@@ -77,7 +84,7 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
     const int32_t ph = jb.phase;
     int64_t a = jb.start, pos = jb.start;            // attempt start, next unread sample
     int32_t lpa = jb.local_phase;                    // localPhase at the attempt start
-    // lane 0's search state (ofdm-processor.cpp:274-338)
+    // the search state, the same in every lane (ofdm-processor.cpp:274-338)
     enum { WARM, INIT, NULLS, ENDNULL };
     int st = WARM, w = 0, idx = 0, counter = 0;
     float sLevel = 0.0f, cur = 0.0f;
@@ -103,148 +110,117 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
 #pragma unroll
             for (int r = 0; r < R; r++) {
                 const int i = lane + 64 * r;
+                float j = 0.0f, h = 0.0f;            // zeros past nb: a group's tail reads them
                 if (i < nb) {
                     const float2 t = cmul_exact(xs[r], os[r]);
-                    const float j = jan_abs(t);
-                    ja[i] = j;
-                    hy[i] = hypotf(t.x, t.y);
-                    pj[i] = 0.00001 * (double)j;
+                    j = jan_abs(t);
+                    h = hypotf(t.x, t.y);
                 }
+                ja[i] = j;
+                hy[i] = h;
+                pj[i] = 0.00001 * (double)j;
             }
         }
         __syncthreads();
-        if (lane == 0) {
-            int kind = 0, at = nb;                   // 0: block consumed, 1: restart after `at`, 2: found at `at`
-            int i = 0;
-            while (i < nb && kind == 0) {
-                if (st == WARM) {                    // 20 T_s samples building sLevel (:280-282)
-                    const int e = min(nb, i + (ACQ_WARM - w));
-                    float sl = sLevel;
-                    int k = i;
-                    for (; k + 8 <= e; k += 8) {
+        // The state machine runs on every lane alike (its state is the same in all 64);
+        // only the two chains of a group run on lane 0 alone.
+        int kind = 0, at = nb;                       // 0: block consumed, 1: restart after `at`, 2: found at `at`
+        int i = 0;
+        while (i < nb && kind == 0) {
+            if (st == WARM) {                        // 20 T_s samples building sLevel (:280-282)
+                const int e = min(nb, i + (ACQ_WARM - w));
+                float sl = sLevel;
+                int k = i;
+                for (; k + 8 <= e; k += 8) {
 #pragma unroll
-                        for (int u = 0; u < 8; u++) sl = slevel_next(sl, pj[k + u]);
-                    }
-                    for (; k < e; k++) sl = slevel_next(sl, pj[k]);
-                    sLevel = sl;
-                    w += e - i;
-                    i = e;
-                    if (w == ACQ_WARM) { st = INIT; idx = 0; cur = 0.0f; }
-                } else if (st == INIT) {             // 50 samples filling the envelope (:286-292)
-                    sLevel = slevel_next(sLevel, pj[i]);
-                    env[idx & 63] = ja[i];
-                    cur += env[idx & 63];
-                    idx++;
-                    i++;
-                    if (idx == ACQ_INIT) { st = NULLS; counter = 0; }
-                } else if (st == NULLS) {            // SyncOnNull (:299-316)
-                    float sl = sLevel, cs = cur;
-                    int k = i;
-                    bool leave = false;
-                    while (k < nb && !leave) {
-                        // the group's inputs in registers (reads past nb stay inside the arrays)
-                        float old[8], vv[8];
-                        double pp[8];
-#pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            old[u] = env[(idx + u - 50) & 63];
-                            vv[u] = ja[k + u];
-                            pp[u] = pj[k + u];
-                        }
-                        if (k + 8 <= nb && counter + 8 <= TF) {
-                            // a whole group: both chains first, then the 8 threshold tests
-                            // side by side (independent), cut at the first that fails
-                            float sv[9], cv[9];
-                            sv[0] = sl;
-                            cv[0] = cs;
-#pragma unroll
-                            for (int u = 0; u < 8; u++) {
-                                sv[u + 1] = slevel_next(sv[u], pp[u]);
-                                cv[u + 1] = cv[u] + (vv[u] - old[u]);
-                            }
-                            int m = 8;
-#pragma unroll
-                            for (int u = 7; u >= 0; u--)
-                                if (!q50_gt(cv[u], 0.40 * (double)sv[u])) m = u;
-                            sl = sv[8];
-                            cs = cv[8];
-#pragma unroll
-                            for (int u = 7; u >= 0; u--) {
-                                if (m == u) { sl = sv[u]; cs = cv[u]; }
-                                if (u < m) env[(idx + u) & 63] = vv[u];
-                            }
-                            idx += m;
-                            k += m;
-                            counter += m;
-                            leave = m < 8;
-                            continue;
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            if (leave || k >= nb) break;
-                            if (!q50_gt(cs, 0.40 * (double)sl)) { leave = true; break; }
-                            sl = slevel_next(sl, pp[u]);
-                            const float v = vv[u];
-                            env[idx & 63] = v;
-                            cs += v - old[u];
-                            idx++;
-                            k++;
-                            if (++counter > TF) {    // hopeless: notSynced
-                                if (jb.scan && attempts > 5) { nosig++; attempts = 0; }
-                                kind = 1; at = k;
-                                leave = true;
-                            }
-                        }
-                    }
-                    sLevel = sl;
-                    cur = cs;
-                    i = k;
-                    if (kind == 0 && k < nb) {       // the dip: SyncOnEndNull (:317-319)
-                        attempts = 0;
-                        counter = 0;
-                        st = ENDNULL;
-                    }
-                } else {                             // SyncOnEndNull (:322-337)
-                    float sl = sLevel, cs = cur;
-                    int k = i;
-                    bool leave = false;
-                    while (k < nb && !leave) {
-                        float old[8], vv[8];
-                        double pp[8];
-#pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            old[u] = env[(idx + u - 50) & 63];
-                            vv[u] = hy[k + u];
-                            pp[u] = pj[k + u];
-                        }
-#pragma unroll
-                        for (int u = 0; u < 8; u++) {
-                            if (leave || k >= nb) break;
-                            if (!q50_lt(cs, 0.75 * (double)sl)) {
-                                kind = 2; at = k;    // end of the null symbol: SyncOnPhase at sample k
-                                leave = true;
-                                break;
-                            }
-                            sl = slevel_next(sl, pp[u]);
-                            const float v = vv[u];
-                            env[idx & 63] = v;
-                            cs += v - old[u];
-                            idx++;
-                            k++;
-                            if (++counter > TNULL + 50) { kind = 1; at = k; leave = true; }
-                        }
-                    }
-                    sLevel = sl;
-                    cur = cs;
-                    i = k;
+                    for (int u = 0; u < 8; u++) sl = slevel_next(sl, pj[k + u]);
                 }
+                for (; k < e; k++) sl = slevel_next(sl, pj[k]);
+                sLevel = sl;
+                w += e - i;
+                i = e;
+                if (w == ACQ_WARM) { st = INIT; idx = 0; cur = 0.0f; }
+            } else if (st == INIT) {                 // 50 samples filling the envelope (:286-292)
+                const int e = min(nb, i + (ACQ_INIT - idx));
+                if (lane < e - i) env[idx + lane] = ja[i + lane];
+                float sl = sLevel, cs = cur;
+                for (int k = i; k < e; k++) {
+                    sl = slevel_next(sl, pj[k]);
+                    cs += ja[k];
+                }
+                sLevel = sl;
+                cur = cs;
+                idx += e - i;
+                i = e;
+                if (idx == ACQ_INIT) { st = NULLS; counter = 0; }
+                __syncthreads();
+            } else {
+                // SyncOnNull (:299-316) / SyncOnEndNull (:322-337) over a group of up to 64
+                // samples: the reference tests the state, then consumes the sample (sLevel
+                // and envelope step, ++counter, give up past the limit).  Lane u forms the
+                // envelope's difference at sample u (the value leaving the window entered 50
+                // samples earlier: the ring before the group, or this group's own sample
+                // u - 50), lane 0 runs both chains over the group, then lane u tests the
+                // state before sample u; the group keeps everything up to the first failure.
+                const bool nulls = st == NULLS;
+                const float *vs = nulls ? ja : hy;
+                const int ng = min(64, nb - i);
+                {
+                    const float v = vs[i + lane];
+                    const float old = lane >= 50 ? vs[i + lane - 50] : env[(idx + lane - 50) & 63];
+                    dd[lane] = lane < ng ? v - old : 0.0f;
+                }
+                __syncthreads();
+                if (lane == 0) {
+                    float sl = sLevel, cs = cur;
+#pragma unroll
+                    for (int u = 0; u < 64; u++) {
+                        sc[u] = make_float2(sl, cs);
+                        sl = slevel_next(sl, pj[i + u]);
+                        cs += dd[u];
+                    }
+                    sc[64] = make_float2(sl, cs);
+                }
+                __syncthreads();
+                const float2 s = sc[lane];
+                const bool pass = nulls ? q50_gt(s.y, 0.40 * (double)s.x)    // still above the dip threshold
+                                        : q50_lt(s.y, 0.75 * (double)s.x);   // still inside the null
+                const uint64_t fails = __ballot(!pass && lane < ng);
+                const int f = fails ? (int)__builtin_ctzll(fails) : ng;
+                const int lim = (nulls ? TF : TNULL + 50) - counter;        // consuming sample `lim` gives up
+                int m;                                                       // samples consumed
+                bool dip = false;
+                if (f < ng && f <= lim) {
+                    m = f;
+                    if (nulls) {                     // the dip: SyncOnEndNull (:317-319)
+                        dip = true;
+                    } else {
+                        kind = 2;                    // end of the null symbol: SyncOnPhase at sample i + f
+                        at = i + f;
+                    }
+                } else if (lim < ng) {
+                    m = lim + 1;                     // hopeless: notSynced
+                    if (nulls && jb.scan && attempts > 5) { nosig++; attempts = 0; }
+                    kind = 1;
+                    at = i + m;
+                } else {
+                    m = ng;
+                }
+                if (lane < m) env[(idx + lane) & 63] = vs[i + lane];
+                const float2 t = sc[m];
+                sLevel = t.x;
+                cur = t.y;
+                idx += m;
+                counter += m;
+                i += m;
+                if (dip) {
+                    attempts = 0;
+                    counter = 0;
+                    st = ENDNULL;
+                }
+                __syncthreads();
             }
-            ev[0] = kind;
-            ev[1] = at;
         }
-        __syncthreads();
-        const int kind = ev[0], at = ev[1];
-        __syncthreads();
         if (kind == 2) {
             pos += at;
             status = 0;
@@ -254,11 +230,9 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
             const int64_t last = pos + at - 1;
             lpa = acq_lp(last, a, lpa, ph);
             a = pos = last + 1;
-            if (lane == 0) {
-                st = WARM; w = 0; idx = 0; cur = 0.0f; sLevel = 0.0f; counter = 0;
-                attempts++;
-                att_start = attempts;
-            }
+            st = WARM; w = 0; idx = 0; cur = 0.0f; sLevel = 0.0f; counter = 0;
+            attempts++;
+            att_start = attempts;
             continue;
         }
         pos += nb;
