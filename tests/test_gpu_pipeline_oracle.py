@@ -366,6 +366,72 @@ def test_scan_mode_counts_attempts_like_reference(ctx):
         diq.free()
 
 
+@pytest.mark.parametrize("scan", [False, True])
+def test_null_search_matches_reference_on_random_streams(ctx, scan):
+    """k_acquire against the reference's null search (ofdm-processor.cpp:274-338,
+    oracle_py.null_scan) on 48 streams cut from a DAB signal at random offsets: some
+    behind a noise prefix (the search gives up after T_F samples and starts over, scan
+    mode counting the attempts), some with a quiet gap (a dip whose end does not come
+    within T_null + 50 samples: notSynced from SyncOnEndNull), some ending early (out of
+    samples inside an attempt).  Every stream's outcome -- synchronised or not, the sample
+    where SyncOnPhase starts, attempts, No_Signal_Found -- equals the reference's, which
+    pins where the 64-sample groups cut: at the first failing threshold test, at the
+    counter limits and at the 1024-sample block ends."""
+    import dabamd
+    from dabamd.synth import Ensemble
+    rng = np.random.default_rng(11 if scan else 12)
+    e = Ensemble(5, snr_db=15.0)
+    sig = e.generate(77, truth=False)["iq"].view(np.complex64)
+    rms = float(np.sqrt(np.mean(np.abs(sig) ** 2)))
+    S, L = 48, 1_300_000
+    streams = np.zeros((S, L), np.complex64)
+    n_avail = []
+    for s in range(S):
+        kind = s % 4
+        off = int(rng.integers(0, 196_608))
+        parts = []
+        if kind == 1:                                 # noise first: at least one give-up
+            z = int(rng.integers(260_000, 520_000))
+            parts.append((rms * (rng.normal(size=z) + 1j * rng.normal(size=z)) / np.sqrt(2)).astype(np.complex64))
+        if kind == 2:                                 # a quiet gap longer than a null
+            g0 = int(rng.integers(60_000, 200_000))
+            gap = int(rng.integers(3_000, 9_000))
+            parts.append(sig[off:off + g0])
+            parts.append((0.01 * rms * rng.normal(size=gap)).astype(np.complex64))
+            off += g0
+        parts.append(sig[off:])
+        x = np.concatenate(parts)[:L]
+        streams[s, :len(x)] = x
+        n = len(x) if kind != 3 else int(rng.integers(40_000, 260_000))
+        n_avail.append(n)
+    iq = streams.view(np.float32)
+    diq = ctx.put(iq)
+    pipe = dabamd.Pipeline(ctx, S, 1, [])
+    try:
+        if scan:
+            pipe.control(dabamd.CTL_SCAN_ON)
+        missing = None
+        try:
+            pipe.acquire(diq, L, [0] * S, n_avail)
+        except dabamd.DabError as ex:              # DABGPU_E_STATE: streams still searching
+            assert "found no null symbol" in str(ex), ex
+            missing = int(str(ex).split(": ")[-1].split()[0])
+        synced = 0
+        for s in range(S):
+            found, att, ns, pos = orc.null_scan(iq[s], n_avail[s], scan)
+            st = pipe.state(s)
+            assert bool(st.synced) == bool(found), (s, st.synced, found)
+            assert (st.attempts, st.no_signal) == (att, ns), (s, st.attempts, st.no_signal, att, ns)
+            if found:
+                assert st.next_pos == pos, (s, st.next_pos, pos)
+            synced += bool(found)
+        assert missing == (S - synced if synced < S else None), (missing, synced)
+        assert synced >= S // 2, synced                 # most streams found a null
+    finally:
+        pipe.close()
+        diq.free()
+
+
 def test_pipeline_iq_display_matches_reference_feed(ctx):
     """the constellation feed (ofdmDecoder::processToken, ofdm-decoder.cpp:192-206): the
     pipeline's symbol-2 display carriers of every 8th frame equal the oracle's iqBuffer
