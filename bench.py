@@ -653,7 +653,10 @@ def main():
                 "traffic": pmc_traffic(demod_kernel, args.workload), "algorithmic_bytes": demod_bytes,
                 "note": "algorithmic bytes: 8*T_s cf32 in + 2K soft bits out as RING8 bytes (ibits + 127; "
                         "SURVEY 8(d)'s 26,560 B/symbol assumes int16 out) per data symbol + 8*T_u of the "
-                        "findIndex window per frame"}
+                        "findIndex window per frame.  ms_per_launch is the launch's span on its stream: the "
+                        "demod is queued once run r-2's ACS is done, so its span includes the time its "
+                        "workgroups wait for the slots the running ACS still holds; frac_alone is the "
+                        "kernel's own rate"}
     roof_hbm["frac"] = roof_hbm["achieved"] / roof_hbm["peak"]
     if tm_alone.get("demod"):
         roof_hbm["ms_per_launch"] = demod_ms

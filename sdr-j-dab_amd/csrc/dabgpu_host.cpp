@@ -850,13 +850,15 @@ struct dabgpu_pipe {
     // vs[r & 1], so run r's back end overlaps run r+1's front end AND run r+1's back
     // end (whose first waves fill the SIMDs run r's last Viterbi waves leave idle).
     // The ring holds 2F+4 frames per stream so run r+1's demod and MSC never touch a
-    // slot run r's MSC still reads; run r+2's front end waits for run r's back end.
+    // slot run r's MSC still reads; run r+2's front end waits for run r's ACS.
     // The caller gives consecutive runs different output buffers (or syncs).
     hipStream_t vs[2] = {nullptr, nullptr};
     int cur = 0;                                // back-end stream of the last run
     hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr}, ev_dp = nullptr;
     bool dp_rec = false;
     bool back_rec[2] = {false, false};
+    hipEvent_t ev_acs[2] = {nullptr, nullptr};  // run r's ACS done (the ring's last reader)
+    bool acs_rec[2] = {false, false};
     int64_t run_idx = 0;
     Profile *ficprof_d = nullptr;
     uint8_t *inv_d = nullptr;        // the subchannel profiles' inverse depuncturing tables
@@ -1037,6 +1039,8 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
                 hipEventCreateWithFlags(&p->ev_back[0], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_back[1], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_copy[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_acs[0], hipEventDisableTiming) != hipSuccess ||
+                hipEventCreateWithFlags(&p->ev_acs[1], hipEventDisableTiming) != hipSuccess ||
                 hipEventCreateWithFlags(&p->ev_copy[1], hipEventDisableTiming) != hipSuccess))
         rc = fail(DABGPU_E_HIP, "pipe stream/event create failed");
     if (!rc) {
@@ -1092,7 +1096,8 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     (void)hipStreamSynchronize(p->c->stream);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamSynchronize(v);
     for (auto e : p->ev_pool) (void)hipEventDestroy(e);
-    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1], p->ev_dp, p->ev_copy[0], p->ev_copy[1]})
+    for (hipEvent_t e : {p->ev_front, p->ev_back[0], p->ev_back[1], p->ev_dp, p->ev_copy[0], p->ev_copy[1],
+                        p->ev_acs[0], p->ev_acs[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
     if (p->as) {                                    // a background null search still running
@@ -1513,10 +1518,12 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
     p->last_info.assign((size_t)S * F, dabgpu_frame_info());
     p->last_msc = nullptr;
     if (p->profiling == 1) p->ev_rec.clear();   // modes 2, 3 accumulate over runs
-    // at most one run of overlap: run r-2's channel decoding must be done before
-    // this run's demod reuses its ring slots
+    // at most one run of overlap: run r-2's ACS, the last reader of the ring slots this
+    // run's demod reuses, must be done (not its traceback, FIC CRC and DAB+ layer: waiting
+    // for those held the demod back from the slots the ACS's last waves leave free --
+    // profiles/r04_front_gate_ab.txt)
     const int par = (int)(p->run_idx & 1);
-    if (p->back_rec[par]) HIPCHK(hipStreamWaitEvent(c->stream, p->ev_back[par], 0));
+    if (p->acs_rec[par]) HIPCHK(hipStreamWaitEvent(c->stream, p->ev_acs[par], 0));
     std::vector<int> done(S, 0);
     std::vector<StreamSt> cur = p->st;
     p->cur = par;
@@ -1602,6 +1609,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
             HIPCHK(launch_acs_msc_fic(bs, JM, JF));
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+            HIPCHK(hipEventRecord(p->ev_acs[par], bs));
+            p->acs_rec[par] = true;
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
             HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
@@ -1611,12 +1620,16 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64
         } else if (fic_bits) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
             HIPCHK(launch_viterbi(bs, JF));
+            HIPCHK(hipEventRecord(p->ev_acs[par], bs));
+            p->acs_rec[par] = true;
             if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         } else if (do_msc) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
             HIPCHK(launch_acs(bs, JM));
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+            HIPCHK(hipEventRecord(p->ev_acs[par], bs));
+            p->acs_rec[par] = true;
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, true));
             HIPCHK(launch_traceback(bs, JM));
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));

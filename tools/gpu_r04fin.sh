@@ -2,7 +2,7 @@
 # Round 4 final build: full -m gpu suite, smoke, the driver's bench command, C5 bench,
 # C3 kernel stats (rocprofv3).
 set -o pipefail
-O=gpurun_out/r04fin; mkdir -p $O
+O=gpurun_out/${OUT:-r04fin}; mkdir -p $O
 export TMPDIR=/tmp
 R=${GRAFT_REPO_ROOT:-/root/repo}
 timeout -k 10 700 python3 -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
