@@ -29,6 +29,8 @@ struct OfdmTables {
     const float *refarg;    // refArg[18] (ofdm-decoder.cpp:71-74)
     const float2 *w2048;    // W2048^j = e^{-2 pi i j/2048}, j < 2048 (double, rounded to float)
     const int16_t *carrier_of_bin;   // [2048] carrier index of an FFT bin (mapper.cpp), -1 if none
+    const int16_t *stage_of_bin;     // [2048] the demod's soft-bit stage word of an FFT bin (stage_layout.h)
+    const int16_t *stage_pair;       // [768] stage word of carrier pair p (carriers 2p, 2p+1)
     int32_t *err;           // device error word: kernels OR in DABGPU_KERR_* bits
 };
 // outputs of the front-end kernels besides the soft bits

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include "../../include/dabgpu.h"
 #include "dab_kernels.h"
+#include "stage_layout.h"
 #include "dab_tables.h"
 
 using namespace dab;
@@ -68,6 +69,7 @@ struct HostTables {
     std::vector<uint32_t> prbs_words;
     std::vector<float2> w2048;
     std::vector<int16_t> carrier_bin;
+    bool stage_ok = true;
     std::vector<float> refarg;
     std::vector<float2> ref;                // natural order refTable
     std::vector<int16_t> perm;              // carrier -> signed carrier (mapIn)
@@ -99,8 +101,39 @@ struct HostTables {
         }
         std::vector<int> carrier_of_bin(2048, -1);
         for (int c = 0; c < 1536; c++) { int k = perm[c]; carrier_of_bin[k < 0 ? k + 2048 : k] = c; }
-        carrier_bin.resize(2048);              // k_demod: carrier of each FFT bin
+        // k_demod: carrier of each FFT bin [2048], then the soft-bit stage words of the
+        // bins [2048] and of the carrier pairs [768] (stage_layout.h)
+        carrier_bin.assign(2048 + 2048 + 768, -1);
         for (int b = 0; b < 2048; b++) carrier_bin[b] = (int16_t)carrier_of_bin[b];
+        {
+            int rank[32] = {};
+            std::vector<int> sig(768);
+            for (int p = 0; p < 768; p++) sig[p] = 32 * rank[STAGE_COL[p]]++ + STAGE_COL[p];
+            for (int r : rank) stage_ok = stage_ok && r == 24;        // a permutation of the 1536 words
+            for (int p = 0; p < 768; p++) carrier_bin[4096 + p] = (int16_t)(2 * sig[p]);
+            // bin b of thread t is b0(t) + 64 k3 (k_demod.hip bin0_of); one store half-wave
+            // = 32 threads of one k3: its dump bins take the banks its carriers leave free
+            auto b0 = [](int t) { const int g = t >> 2, tq = t & 3; return (g >> 3) + 8 * (g & 7) + 512 * (((tq & 1) << 1) | (tq >> 1)); };
+            for (int h = 0; h < 8; h++)
+                for (int k3 = 0; k3 < 8; k3++) {
+                    bool used[32] = {};
+                    for (int l = 0; l < 32; l++) {
+                        const int b = b0(32 * h + l) + 64 * k3, cc = carrier_of_bin[b];
+                        if (cc < 0) continue;
+                        const int w = 2 * sig[cc >> 1] + (cc & 1);
+                        carrier_bin[2048 + b] = (int16_t)w;
+                        used[w & 31] = true;
+                    }
+                    int nb = 0;
+                    for (int l = 0; l < 32; l++) {
+                        const int b = b0(32 * h + l) + 64 * k3;
+                        if (carrier_of_bin[b] >= 0) continue;
+                        while (nb < 31 && used[nb]) nb++;
+                        used[nb] = true;
+                        carrier_bin[2048 + b] = (int16_t)(1536 + nb);
+                    }
+                }
+        }
         w2048.resize(2048);                    // k_demod twiddles
         for (int j = 0; j < 2048; j++) {
             const double ph = -2.0 * M_PI * j / 2048.0;
@@ -420,6 +453,10 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     }
     for (auto &e : c->ev) HIPCHK(hipEventCreate(&e));
     const HostTables &t = host_tables();
+    if (!t.stage_ok) {
+        dabgpu_ctx_destroy(c);
+        return fail(DABGPU_E_STATE, "stage_layout.h: STAGE_COL is not 24 pairs per colour");
+    }
     int rc = 0;
     if ((rc = upload(c, &c->osc, t.osc)) || (rc = upload(c, &c->nco, t.nco)) || (rc = upload(c, &c->ref, t.ref)) ||
         (rc = upload(c, &c->w2048, t.w2048)) || (rc = upload(c, &c->carrier_bin, t.carrier_bin)) ||
@@ -434,6 +471,8 @@ int dabgpu_ctx_create(int device, dabgpu_ctx **out) {
     c->T.ref = c->ref;
     c->T.w2048 = c->w2048;
     c->T.carrier_of_bin = c->carrier_bin;
+    c->T.stage_of_bin = c->carrier_bin + 2048;
+    c->T.stage_pair = c->carrier_bin + 4096;
     c->T.refarg = c->refarg;
     if (hipMalloc((void **)&c->err, sizeof(int32_t)) != hipSuccess || hipMemset(c->err, 0, sizeof(int32_t)) != hipSuccess ||
         hipHostMalloc((void **)&c->h_err, sizeof(int32_t), hipHostMallocDefault) != hipSuccess) {

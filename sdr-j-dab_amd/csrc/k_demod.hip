@@ -335,9 +335,14 @@ __device__ __forceinline__ void soft_pair(float2 r1, float ab1, int &ir, int &ii
 }
 
 // The soft bits of symbol l leave through an LDS stage of 1536 {re, im} int16 pairs
-// (one 32-bit write per carrier), read back by carrier quads as 16-byte words and
-// stored as 8-byte re / im groups: output rows stay [3072] = re[1536] | im[1536].
-constexpr int STG = K + DT;                              // + one dump slot per thread
+// (one 32-bit write per carrier), read back by carrier quads (two 8-byte pair reads) and
+// stored as re / im groups: output rows stay [3072] = re[1536] | im[1536].  The stage
+// keeps carriers in pairs at host-chosen words (T.stage_of_bin, T.stage_pair;
+// stage_layout.h): the de-interleave's scattered stores then hit distinct banks in each
+// 32-lane half (3 two-way collisions per symbol, the lower bound, instead of 158 extra
+// cycles), and each pair read covers the 64 banks.  Bins that carry nothing write to 32
+// dump words, each store half-wave's at banks its carriers leave free.
+constexpr int STG = K + 32;
 
 template <bool GEN, bool SYNC, bool R8>
 __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2 *__restrict__ iq,
@@ -408,17 +413,20 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     if (!ok && !skip && t == 0) atomicOr(T.err, KERR_FRAME);
     if (l0 <= NSYM && ok && !skip) {
         const int64_t dorg = fr.block0 + TU;           // first sample of segment B
-        // LDS stage byte address of each of this thread's 8 bins (its carrier's slot, or
-        // the thread's dump slot K + t for a bin that carries nothing), two u16 per register
-        uint32_t cb[4];
+        // LDS stage byte address of each of this thread's 8 bins (its carrier's word, or a
+        // dump word for a bin that carries nothing), two u16 per register, and the stage
+        // words of the carrier pairs its read-back quads q = t, t + DT take
+        uint32_t cb[4], rq[2];
         {
             const int b0 = bin0_of(t);
-            auto slot = [&](int k3) -> uint32_t {
-                const int c = T.carrier_of_bin[b0 + 64 * k3];
-                return (uint32_t)(c >= 0 ? c : K + t) * 4u;
-            };
+            auto slot = [&](int k3) -> uint32_t { return (uint32_t)T.stage_of_bin[b0 + 64 * k3] * 4u; };
 #pragma unroll
             for (int k3 = 0; k3 < 8; k3 += 2) cb[k3 >> 1] = slot(k3) | (slot(k3 + 1) << 16);
+#pragma unroll
+            for (int i = 0; i < 2; i++) {
+                const int q = t + DT * i;
+                rq[i] = q < K / 4 ? (uint32_t)T.stage_pair[2 * q] | ((uint32_t)T.stage_pair[2 * q + 1] << 16) : 0u;
+            }
         }
         // the frame's samples and soft-bit rows through buffer descriptors (wave-uniform
         // bases: 32-bit offsets, the 8 samples of a thread a scalar offset apart, no
@@ -573,11 +581,11 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             }
             if (softf) {                               // parity tests only: the float soft values
                 float *sf = softf + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS;
+                const int b0 = bin0_of(t);
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
-                    const int c = (int)(addr >> 2);
-                    if (c < K) {
+                    const int c = T.carrier_of_bin[b0 + 64 * k];
+                    if (c >= 0) {
                         const float2 r1 = cmul_conj_exact(a[k], P[k]);
                         const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                         sf[c] = -r1.x / ab1;
@@ -590,17 +598,29 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             __syncthreads();
             // carriers 4q..4q+3, q < 384: re to row[4q..], im to row[K + 4q..]
             const int32_t rowb = (l - 1) * SYMBITS * esz;
+            // carriers 4q, 4q+1 and 4q+2, 4q+3: two pair words of the stage
+            auto quad = [&](int i) {
+                const uint2 a = *(const uint2 *)(st + (rq[i] & 0xFFFFu));
+                const uint2 b = *(const uint2 *)(st + (rq[i] >> 16));
+                return make_uint4(a.x, a.y, b.x, b.y);
+            };
             if constexpr (R8) {                        // the low bytes of each half
-                for (int q = t; q < K / 4; q += DT) {
-                    const uint4 w = ((const uint4 *)st)[q];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int q = t + DT * i;
+                    if (q >= K / 4) break;
+                    const uint4 w = quad(i);
                     const uint32_t xy = __builtin_amdgcn_perm(w.y, w.x, 0x06040200u);   // re0 im0 re1 im1
                     const uint32_t zw = __builtin_amdgcn_perm(w.w, w.z, 0x06040200u);   // re2 im2 re3 im3
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(zw, xy, 0x06040200u), rout, rowb + 4 * q, 0, 0);
                     __builtin_amdgcn_raw_buffer_store_b32(__builtin_amdgcn_perm(zw, xy, 0x07050301u), rout, rowb + K + 4 * q, 0, 0);
                 }
             } else {
-                for (int q = t; q < K / 4; q += DT) {
-                    const uint4 w = ((const uint4 *)st)[q];
+#pragma unroll
+                for (int i = 0; i < 2; i++) {
+                    const int q = t + DT * i;
+                    if (q >= K / 4) break;
+                    const uint4 w = quad(i);
                     const uint2 re = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x05040100u),
                                                 __builtin_amdgcn_perm(w.w, w.z, 0x05040100u));
                     const uint2 im = make_uint2(__builtin_amdgcn_perm(w.y, w.x, 0x07060302u),
