@@ -16,17 +16,19 @@ superframe grid wrap around the period, so the stream is valid across the seams 
 the decoder does the same work everywhere; synthesis costs P frames per ensemble
 instead of the whole run's.
 
+The streams sit in HBM as recorded samples (--iq-format: s16 = .sdr PCM16 by default,
+f32, u8 = .raw) that the kernels convert exactly in their loads.
+
 Multi-GPU (C4): one process per GPU.  `python bench.py --gpus N` starts the N ranks
 itself (torch.distributed.run, 127.0.0.1) unless it already runs under a launcher.
---iq-source local (default): each rank generates its own ensembles (seeded by rank)
-straight into its HBM -- no data-path collective, weak scaling.  --iq-source rccl:
-rank 0 holds every rank's (distinct) ensembles as int16 .sdr samples and sends each
-rank chunk k of ITS streams per step with grouped send/recv over RCCL (xGMI) while the
-ranks decode the previous chunk (StreamSplit); the receivers convert the samples to
-cf32 on the GPU (dabgpu_iq_convert).  With N > 1 the default run also measures that
-transfer on its own ("stream_split"), so the link-bound rate is reported beside the
-rank-local one.  Every rank checks one step of its ensemble 0 against the transmitted
-bits.  value = symbols decoded by all ranks / max-over-ranks time.
+value: each rank decodes its own ensembles (seeded by rank) from its own HBM -- no
+data-path collective, weak scaling.  Then the "c4_fed" leg runs BASELINE configs[3] as
+named: rank 0 holds every rank's recorded streams (--fed-format, u8 .raw by default) and
+sends each rank chunk k + 2 of ITS streams over RCCL (xGMI) while step k decodes
+(FedSplit); the receivers' pipelines read the samples in place.  It is link-bound by
+design and reported beside value.  Every rank checks one step of its
+ensemble 0 against the transmitted bits in both legs.  value = symbols decoded by all
+ranks / max-over-ranks time.
 """
 import argparse
 import json
@@ -125,13 +127,34 @@ def allreduce_max(dist, x):
     return float(t.item())
 
 
-# --------------------------------------------------------------- stream split
+# ------------------------------------------------------------ sample formats
+# recorded-IQ formats the pipeline reads straight from HBM (dabgpu_pipe_set_iq_format):
+# name -> (DABGPU_IQ_* code, bytes per I/Q pair, numpy dtype of one value)
+FORMATS = {"f32": (0, 8, np.float32), "u8": (1, 2, np.uint8), "s16": (2, 4, np.int16)}
+FORMAT_DESC = {"f32": "cf32 (virtualInput::getSamples' DSPCOMPLEX)",
+               "s16": ".sdr PCM16 (wavfiles.cpp:172: x / 32768, converted in the kernels' loads)",
+               "u8": ".raw u8 (rawfiles.cpp:115-117: float(x - 128) / 128, converted in the kernels' loads)"}
+# transmitter amplitude of the synthetic streams: peaks inside +-1, as a recording's gain
+# sets them (unit-power OFDM at 1.0 would clip in the PCM16 / u8 formats)
+AMPLITUDE = 0.25
+
+
+def to_raw(iq, fmt):
+    """cf32 IQ -> the samples of a recorded format: s16 round(32768 x), u8 round(128 x + 128),
+    clipped to the format's range (what the readers turn back into x exactly)"""
+    x = np.asarray(iq, np.float32)
+    if fmt == "s16":
+        return np.clip(np.rint(x * 32768.0), -32768, 32767).astype(np.int16)
+    if fmt == "u8":
+        return np.clip(np.rint(x * 128.0 + 128.0), 0, 255).astype(np.uint8)
+    return x
+
+
 def to_s16(iq):
-    """cf32 IQ -> interleaved int16 as an .sdr recording stores it (x * 32768, rounded,
-    clipped): the receivers' dabgpu_iq_convert(DABGPU_IQ_S16) gives x back to 2^-15"""
-    return np.clip(np.rint(np.asarray(iq, np.float32) * 32768.0), -32768, 32767).astype(np.int16)
+    return to_raw(iq, "s16")
 
 
+# --------------------------------------------------------------- stream split
 def chunk_layout(stream_len, F):
     """samples per stream chunk (F frames) and the number of chunks covering a stream"""
     cs = F * TF
@@ -148,54 +171,91 @@ def period_frames(F, dabplus):
     return F * m
 
 
-def chunk_phases(ens, P, cs, E, seed0, threads):
-    """int16 IQ (.sdr samples) of E cyclic streams (seeds seed0 + e) as the P * TF / cs
-    distinct stream chunks: [phase j][ensemble][2 * cs] = stream samples [j cs, (j+1) cs),
-    which chunk k = j + i P/F repeats."""
+def fill_chunk_phases(out, per, ens, P, cs, g0, fmt):
+    """out[j, g0 + e] = stream samples [j cs, (j+1) cs) of the cyclic stream whose period
+    is per[e] (interleaved cf32), as format fmt -- chunk k of the stream is phase k % m"""
+    for j in range(out.shape[0]):
+        for p, q, c in ens.stream_pieces(P, j * cs, cs):
+            o = p - j * cs
+            out[j, g0:g0 + len(per), 2 * o:2 * (o + c)] = to_raw(per[:, 2 * q:2 * (q + c)], fmt)
+
+
+def chunk_phases(ens, P, cs, E, seed0, threads, fmt="s16"):
+    """the P * TF / cs distinct stream chunks of E cyclic streams (seeds seed0 + e) in a
+    recorded format: [phase j][ensemble][2 * cs] values"""
     m = P * TF // cs
-    out = np.zeros((m, E, 2 * cs), np.int16)
+    out = np.zeros((m, E, 2 * cs), FORMATS[fmt][2])
     for g0 in range(0, E, 8):
         n = min(8, E - g0)
-        per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
-        for j in range(m):
-            for p, q, c in ens.stream_pieces(P, j * cs, cs):
-                o = p - j * cs
-                out[j, g0:g0 + n, 2 * o:2 * (o + c)] = to_s16(per[:, 2 * q:2 * (q + c)])
-        del per
+        fill_chunk_phases(out, ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads), ens, P, cs, g0, fmt)
     return out
 
 
-class StreamSplit:
-    """The C4 stream split (BASELINE configs[3]): rank 0 holds every rank's
-    streams and, per step, sends rank r (r >= 1) chunk k of rank r's own ensembles in one
-    grouped send/recv (ncclGroupStart/End under RCCL over xGMI).  src (rank 0): per
-    destination rank an int16 tensor [phases][E][2 * cs] (chunk_phases); chunk k is phase
-    k % phases.  begin(k) starts moving chunk k; end(k, reqs) waits and returns this
-    rank's [E][2 * cs] chunk (None past the last chunk)."""
+def p2p_batch(dist, sends, recvs):
+    """One grouped batch of point-to-point transfers, sends / recvs = [(tensor, peer)], in
+    posting order per peer.  Under RCCL ("nccl") one ncclGroupStart/End: every transfer
+    on its own xGMI link, received in place.  Under gloo with device tensors (ranks sharing
+    one GPU: the rehearsal of this path) staged through host copies.  Returns waitables."""
+    import torch
+    import torch.distributed as td
+    staged = td.get_backend() == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs))
+    if not staged:
+        ops = [td.P2POp(td.isend, t, p) for t, p in sends] + [td.P2POp(td.irecv, t, p) for t, p in recvs]
+        return td.batch_isend_irecv(ops) if ops else []
+    hs = [(t.cpu(), p) for t, p in sends]
+    hr = [(torch.empty(t.shape, dtype=t.dtype), t, p) for t, p in recvs]
+    ops = [td.P2POp(td.isend, h, p) for h, p in hs] + [td.P2POp(td.irecv, h, p) for h, _, p in hr]
+    reqs = td.batch_isend_irecv(ops) if ops else []
 
-    def __init__(self, dist, rank, world, E, cs, phases, nchunks, device, src=None):
-        import torch
-        self.dist, self.rank, self.world, self.phases, self.nchunks = dist, rank, world, phases, nchunks
-        self.src = src
-        self.recv = torch.zeros((E, 2 * cs), dtype=torch.int16, device=device) if rank else None
+    class _Staged:
+        def wait(self):
+            for q in reqs:
+                q.wait()
+            for h, t, _ in hr:
+                t.copy_(h)
+    return [_Staged()]
+
+
+class FedSplit:
+    """The C4 stream split (BASELINE configs[3]: "512 ensembles sharded across
+    8 MI355X via RCCL ... of IQ chunks over xGMI").  Rank 0 holds every rank's recorded
+    streams: src[r] = [phases][E][2 * cs] values of rank r's ensembles.  begin(k) moves
+    chunk k of every stream of every rank r >= 1 from rank 0 straight into rank r's stream
+    buffer -- dst(e, k) is the [2 * cs] view of stream e's samples [k cs, (k+1) cs) -- as
+    one grouped batch (E sends per destination on rank 0, E receives on each rank: a
+    scatter, each destination over its own link, not a ring broadcast of all 512
+    ensembles); end(reqs) waits for it.  Rank 0 reads its own streams in place."""
+
+    def __init__(self, dist, rank, world, E, phases, src=None, dst=None):
+        self.dist, self.rank, self.world, self.E, self.phases = dist, rank, world, E, phases
+        self.src, self.dst = src, dst
 
     def begin(self, k):
-        if k >= self.nchunks:
-            return None
-        sends = [s[k % self.phases] for s in self.src] if self.rank == 0 else None
-        return scatter_chunk(self.dist, self.rank, self.world, sends, self.recv)
+        if self.rank == 0:
+            sends = [(self.src[r][k % self.phases][e], r) for r in range(1, self.world) for e in range(self.E)]
+            return p2p_batch(self.dist, sends, [])
+        return p2p_batch(self.dist, [], [(self.dst(e, k), 0) for e in range(self.E)])
 
-    def end(self, k, reqs):
-        if k >= self.nchunks:
-            return None
+    def end(self, reqs):
         for r in reqs or []:
             r.wait()
-        if self.rank == 0:
-            return self.src[0][k % self.phases]
-        if self.recv.is_cuda:
-            import torch
-            torch.cuda.current_stream().synchronize()
-        return self.recv
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.current_stream().synchronize()       # the chunk has landed before a run reads it
+
+
+def gather_to_rank0(dist, rank, world, mine):
+    """setup (untimed): every rank's chunk phases to rank 0 (one transfer per rank);
+    returns the list [rank 0's, rank 1's, ...] on rank 0, None elsewhere"""
+    import torch
+    if rank == 0:
+        got = [mine] + [torch.empty_like(mine) for _ in range(1, world)]
+        for r in p2p_batch(dist, [], [(got[q], q) for q in range(1, world)]):
+            r.wait()
+        return got
+    for r in p2p_batch(dist, [(mine, 0)], []):
+        r.wait()
+    return None
 
 
 def check_step(truth, P, st0, st1, fic, crc, msc, valid, subch):
@@ -229,38 +289,6 @@ def gather_objects(dist, obj):
     return out
 
 
-def scatter_chunk(dist, rank, world, sends, recv):
-    """Stream split: rank 0 sends sends[r] (a tensor) to rank r (r >= 1) as one grouped
-    send/recv (ncclGroupStart/End under RCCL; batched p2p under gloo); ranks >= 1
-    receive into `recv`.  Returns the request list (wait on it)."""
-    import torch.distributed as td
-    staged = td.get_backend() == "gloo" and ((recv is not None and recv.is_cuda) or
-                                             (sends is not None and sends[-1].is_cuda))
-    if staged:
-        # gloo (ranks sharing one GPU: a rehearsal of this path) moves host tensors only
-        ops = []
-        if rank == 0:
-            for r in range(1, world):
-                ops.append(td.P2POp(td.isend, sends[r].cpu(), r))
-            return td.batch_isend_irecv(ops)
-        host = recv.new_empty(recv.shape, device="cpu")
-        reqs = td.batch_isend_irecv([td.P2POp(td.irecv, host, 0)])
-
-        class _Staged:
-            def wait(self):
-                for q in reqs:
-                    q.wait()
-                recv.copy_(host)
-        return [_Staged()]
-    ops = []
-    if rank == 0:
-        for r in range(1, world):
-            ops.append(td.P2POp(td.isend, sends[r], r))
-    else:
-        ops.append(td.P2POp(td.irecv, recv, 0))
-    return td.batch_isend_irecv(ops) if ops else []
-
-
 # ----------------------------------------------------------------- CPU side
 def pmc_traffic(kernel, workload):
     """HBM bytes per full-batch launch of `kernel` from the newest committed PMC
@@ -289,10 +317,24 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_quota():
+    """the cgroup's CPU quota in cores (cpu.max), or None when unlimited / unreadable"""
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        return None if q == "max" else float(q) / float(per)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_cores():
-    """the cores this process may use (the GPU box's CPU share: OMP_NUM_THREADS caps it)"""
+    """the cores the workers run on: the process's affinity set, capped at the box's CPU
+    share (OMP_NUM_THREADS, which the GPU box sets to its share, and the cgroup quota) --
+    more workers than the share only time-slice the same cores"""
     cores = sorted(os.sched_getaffinity(0))
     cap = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    q = cpu_quota()
+    if q is not None:
+        cap = min(cap, int(q)) if cap > 0 else int(q)
     return cores[:cap] if cap > 0 else cores
 
 
@@ -300,8 +342,8 @@ def cpu_baseline(frames=20, budget_s=20.0, workload="c3", cfo=0.0):
     """The reference CPU path on the host cores: one worker process per
     core, pinned (sched_setaffinity = taskset), each decoding its own synthetic ensemble
     of the workload for a bounded time.  Stages: OFDM front end = the oracle's C
-    restatement of ofdmProcessor::run/ofdmDecoder (FFTW3f absent: its FFT is a
-    double-precision radix-2 stand-in); FIC = restated depuncture + the reference's
+    restatement of ofdmProcessor::run/ofdmDecoder with the reference's oscillatorTable and
+    an fp32 radix-4 FFT (orc_fft2048_f32: FFTW3f, absent here, is an fp32 transform); FIC = restated depuncture + the reference's
     viterbi.cpp + spiral-sse.c + check_CRC_bits; MSC = restated 16-CIF de-interleave +
     the reference's deconvolve.cpp (UEP/EEP + Viterbi) + PRBS; DAB+ = the reference's
     firecode_checker + reedSolomon inside the restated mp4Processor glue
@@ -326,7 +368,8 @@ def cpu_baseline(frames=20, budget_s=20.0, workload="c3", cfo=0.0):
     # chain is labelled a port; its FIC/MSC/DAB+ back end is the reference's own code
     kind = "port"
     return dict(value=tot["symbols"] / secs, cores=len(cores), kind=kind, tot=tot, secs=secs,
-                nproc=os.cpu_count(), cpu=cpu_model())
+                nproc=os.cpu_count(), cpu=cpu_model(), affinity=len(os.sched_getaffinity(0)),
+                omp=os.environ.get("OMP_NUM_THREADS"), quota=cpu_quota())
 
 
 def _cpu_worker(w, core, frames, budget_s, q, workload, cfo):
@@ -355,7 +398,7 @@ def _cpu_worker(w, core, frames, budget_s, q, workload, cfo):
     t0 = time.perf_counter()
     while True:
         a = time.perf_counter()
-        n, info, soft = orc.ofdm_run(g["iq"], frames + 4)
+        n, info, soft = orc.ofdm_run(g["iq"], frames + 4, fft_kind=1)
         b = time.perf_counter()
         st["t_ofdm"] += b - a
         for f in range(n):                               # ficHandler: 4 blocks per frame
@@ -410,6 +453,23 @@ def _cpu_worker(w, core, frames, budget_s, q, workload, cfo):
 
 
 # ----------------------------------------------------------------------- main
+def acs_clock_issue():
+    """The ACS's achieved clock and VALU issue utilisation from the newest committed PMC
+    summary (profiles/rNN_acs_clock_issue.json, tools/acs_clock_issue.py over one
+    rocprofv3 --pmc pass of this bench command: GRBM_GUI_ACTIVE / 8 / kernel duration and
+    4 x SQ_ACTIVE_INST_VALU / (1024 SIMDs x cycles)), or None."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_acs_clock_issue.json")))
+    if not files:
+        return None
+    try:
+        d = json.load(open(files[-1]))
+    except (OSError, ValueError):
+        return None
+    d["source"] = os.path.basename(files[-1])
+    return d
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -423,7 +483,15 @@ def main():
     ap.add_argument("--cfo", type=float, default=1300.0,
                     help="carrier frequency offset of the synthetic IQ (Hz); nonzero by default: a receiver's NCO "
                          "always runs (phase = coarse + fine correction), 0 takes the constant-phase shortcut")
-    ap.add_argument("--iq-source", choices=["local", "rccl"], default="local")
+    ap.add_argument("--iq-format", choices=["s16", "f32", "u8"], default="s16",
+                    help="how the streams sit in HBM: s16 = .sdr PCM16 samples (default; SURVEY 8(d)'s int16 "
+                         "transport), f32 = cf32, u8 = .raw samples -- read by the kernels through "
+                         "dabgpu_pipe_set_iq_format, converted exactly in their loads")
+    ap.add_argument("--fed-format", choices=["u8", "s16"], default="u8",
+                    help="the C4 stream split's wire format (N > 1): u8 = .raw (2 B per sample over xGMI)")
+    ap.add_argument("--fed-steps", type=int, default=8,
+                    help="timed steps of the C4 leg (N > 1): rank 0 feeding every rank its ensembles over RCCL")
+    ap.add_argument("--no-c4-fed", action="store_true", help="skip the C4 leg when N > 1")
     ap.add_argument("--msc-format", choices=["bits", "packed"], default="packed",
                     help="MSC output of the timed steps: one bit per byte as the reference's deconvolve delivers it "
                          "(viterbi.cpp:240-241), or 8 bits per byte (dabgpu_pipe_set_packed; the DAB+ layer reads "
@@ -456,91 +524,57 @@ def main():
     SUBCH, E_default, wl_desc = WORKLOADS[args.workload]
     dabplus = any(s[5] for s in SUBCH)
     E, F = args.ensembles or E_default, args.frames
+    fmt_code, bps, _ = FORMATS[args.iq_format]
     # +1 step: the checked pass; then the solo steps
     deliv_steps = args.delivered_steps + 1 if args.delivered_steps > 0 else 0     # + one untimed warm-up
     loss_steps = 2 * (args.sync_loss_steps + 1) if args.sync_loss_steps > 0 else 0  # two modes, + one each
     # (+ 2F: a stream that loses sync skips frames and reaches the end of its samples sooner)
     total_frames = F * (args.warmup + args.steps + 1 + args.solo_steps + deliv_steps + loss_steps + (2 if loss_steps else 0)) + 1
-    ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0, cfo_hz=args.cfo)
+    ens = Ensemble(total_frames, subch=SUBCH, snr_db=30.0, cfo_hz=args.cfo, amplitude=AMPLITUDE)
     P = period_frames(F, dabplus)
     ctx = dabamd.Context(rank_device(local))
     stride = ens.length
-    rccl = args.iq_source == "rccl" and world > 1
     threads = min(16, os.cpu_count() or 1)
+    fed = world > 1 and not args.no_c4_fed
+    cs, _ = chunk_layout(stride, F)
+    fed_ph = np.zeros((P * TF // cs, E, 2 * cs), FORMATS[args.fed_format][2]) if fed else None
     # Every stream is cyclic (dabsynth_generate_period: P frames repeated end to end, a
-    # valid DAB stream across the seams); ensemble 0 of each rank is generated with its
-    # transmitted bits for the checked step.
+    # valid DAB stream across the seams), stored in HBM as the chosen recorded format;
+    # ensemble 0 of each rank is generated with its transmitted bits for the checked step.
     t0 = time.time()
-    diq = ctx.buf(E * 2 * stride * 4)
+    diq = ctx.buf(E * stride * bps)
     seed0 = rank_seed0(rank, E)
-    cs, nchunks = chunk_layout(stride, F)
     truth = ens.generate_period(seed0, P, truth=True)
     truth.pop("iq")
-    split = None
-    if rccl:
-        import torch
-        dev = f"cuda:{rank_device(local)}"
-        src = None
-        if rank == 0:
-            # rank 0 holds every rank's streams as int16 (.sdr samples), one period each,
-            # as the P / F distinct chunk phases [phase][ensemble][2 * cs]
-            src = [torch.from_numpy(chunk_phases(ens, P, cs, E, rank_seed0(r, E), threads)).to(dev)
-                   for r in range(world)]
-        split = StreamSplit(dist, rank, world, E, cs, P // F, nchunks, dev, src)
-    else:
-        for g0 in range(0, E, 8):
-            n = min(8, E - g0)
-            per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
-            for e in range(n):
-                for p, q, m in ens.stream_pieces(P):
-                    diq.upload_at(per[e, 2 * q:2 * (q + m)], ((g0 + e) * 2 * stride + 2 * p) * 4)
-            del per
+    for g0 in range(0, E, 8):
+        n = min(8, E - g0)
+        per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
+        for e in range(n):
+            for p, q, m in ens.stream_pieces(P):
+                diq.upload_at(to_raw(per[e, 2 * q:2 * (q + m)], args.iq_format), ((g0 + e) * stride + p) * bps)
+        if fed:
+            fill_chunk_phases(fed_ph, per, ens, P, cs, g0, args.fed_format)
+        del per
     gen_s = time.time() - t0
     subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, dabamd.SUBCH_DABPLUS if s[5] else 0)
             for s in SUBCH]
     pipe = dabamd.Pipeline(ctx, E, F, subs)
+    pipe.set_iq_format(fmt_code)
     if args.msc_format == "packed":
         pipe.set_packed(True)
-
-    # stream split over RCCL: chunk k of every stream from rank 0 to each rank, converted
-    # into this rank's cf32 stream buffer on the GPU
-    got = [0]                                             # chunks available on this rank
-
-    def feed_end(k, reqs):
-        chunk = split.end(k, reqs)
-        if chunk is None:
-            return
-        m = min(cs, stride - k * cs)
-        for e in range(E):
-            ctx.iq_convert(dabamd.IQ_S16, _TorchBuf(chunk[e]), m, diq, dst_off=(e * 2 * stride + 2 * k * cs) * 4)
-        ctx.sync()                                        # the receive buffer is reused by the next chunk
-        got[0] = k + 1
-    if rccl:
-        torch.cuda.synchronize()
-        for k in range(2):
-            feed_end(k, split.begin(k))
-
-    def avail():
-        if not rccl:
-            return [stride] * E
-        return [min(stride, got[0] * cs)] * E
 
     # the initial null search of every stream (k_acquire, one wave per stream): the cost a
     # sync loss pays before the pipeline resumes (ofdm-processor.cpp:298-357), reported beside
     # the steady state, never inside the timed region
     pipe.sync()
     t_acq = time.perf_counter()
-    pipe.acquire(diq, stride, [0] * E, avail())
+    pipe.acquire(diq, stride, [0] * E, [stride] * E)
     pipe.sync()
     acquire_ms = (time.perf_counter() - t_acq) * 1e3
 
     def step(k, download=False):
-        # chunk k + 2 travels while step k decodes (the frames of step k need chunks <= k + 1)
-        reqs = split.begin(k + 2) if rccl else None
-        r = pipe.run(diq, stride, avail(), download=download)
+        r = pipe.run(diq, stride, [stride] * E, download=download)
         d = pipe.dabplus(download=download) if dabplus else None
-        if rccl:
-            feed_end(k + 2, reqs)
         return r, d
 
     for i in range(args.warmup):
@@ -590,29 +624,28 @@ def main():
     # packed 8 bits per byte, DAB+ superframe records + bytes) into pinned host memory,
     # each copy queued behind its run's channel decoding while the next run decodes
     delivered = None
-    if deliv_steps and not rccl:
+    if deliv_steps:
         k0 = ck + 1 + args.solo_steps
         delivered = delivered_leg(dabamd, ctx, pipe, step, k0, deliv_steps - 1, E, F, SUBCH, dabplus, dist, truth, P)
     sync_loss = None
-    if loss_steps and not rccl and E >= 2:
+    if loss_steps and E >= 2:
         k0 = ck + 1 + args.solo_steps + deliv_steps
         sync_loss = sync_loss_leg(dabamd, ctx, pipe, step, k0, args.sync_loss_steps, E, F, stride, diq, dist,
-                                  el / args.steps * 1e3)
+                                  el / args.steps * 1e3, args.iq_format)
     sf_ok = None
     if dp is not None:
         info = dp[0]
         sf_ok = {"superframes": int((info["status"] == 3).sum()),
                  "au_crc_pass": int(sum(bin(int(x)).count("1") for x in info["au_crc_ok"][info["status"] == 3])),
                  "cif_records": int((info["status"] >= 0).sum())}
-
     symbols = world * E * F * 76 * args.steps
     value = symbols / el
-    probe = None
-    if world > 1 and not rccl:
-        try:
-            probe = stream_split_probe(dist, rank, world, local, E, F)
-        except Exception as e:                          # never costs the main measurement
-            probe = {"error": repr(e)[:300]}
+    c4 = None
+    if fed:
+        pipe.close()
+        diq.free()
+        c4 = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs, fed_ph,
+                        args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
     if rank != 0:
         return
     # dominant kernel + its roofline.  Launches overlap in the pipeline (the next run's
@@ -629,10 +662,10 @@ def main():
     acs_ms = max(tm[acs_stage][1], 1e-9)            # average launch duration
     acs_ops = acs_steps * 64 * 4                    # 2 adds + compare + select per ACS
     demod_ms = max(tm["demod"][1], 1e-9)
-    # cf32 in + the pipeline's RING8 soft bits out (one byte each: ibits + 127) + the
-    # findIndex window; SURVEY 8(d)'s 26,560 B/symbol counts int16 soft bits out
-    demod_bytes = E * F * (75 * (8 * TS + 3072) + 8 * TU)
-    demod_kernel = "dab::k_demod_wg<true, true, true>" if args.cfo else "dab::k_demod_wg<false, true, true>"
+    # the recorded samples in + the pipeline's RING8 soft bits out (one byte each: ibits +
+    # 127) + the findIndex window; SURVEY 8(d)'s 26,560 B/symbol counts cf32 in, int16 out
+    demod_bytes = E * F * (75 * (bps * TS + 3072) + bps * TU)
+    demod_kernel = "dab::k_demod_wg<%s, true, true, %d, false>" % ("true" if args.cfo else "false", fmt_code)
     roof_valu = {"kernel": f"{acs_kernel[5:]} (Viterbi ACS)", "bound": "valu",
                  "achieved": acs_ops / (acs_ms * 1e-3) / 1e12, "peak": VALU_PEAK_TOPS, "unit": "TOP/s",
                  "traffic": pmc_traffic(acs_kernel, args.workload),
@@ -640,10 +673,18 @@ def main():
                          "32 lanes x 2.4 GHz (the 32-bit rate). Formulation ceiling ~0.6 of it: the exact u16x2 ACS "
                          "word is 6 VALU per wave-step (2 codeword steps = 512 ops), of which the packed-16, DPP, "
                          "v_perm and v_bfi ops issue at half rate (profiles/r02_valu_rate.txt), ~24 issue cycles + "
-                         "~2 for the loader: 512 / 26 / 32 = 0.62 at 100 % issue; frac_of_ceiling = frac / 0.62",
+                         "~2 for the loader: 512 / 26 / 32 = 0.62 at 100 % issue; frac_of_ceiling = frac / 0.62.  "
+                         "clock_ghz / issue_utilisation: the kernel's PMC pass (GRBM_GUI_ACTIVE / 8 / duration; "
+                         "4 SQ_ACTIVE_INST_VALU / (1024 SIMDs x cycles)); frac_at_clock = frac x 2.4 / clock_ghz",
                  "formulation_ceiling_frac": 0.62}
     roof_valu["frac"] = roof_valu["achieved"] / roof_valu["peak"]
     roof_valu["frac_of_ceiling"] = roof_valu["frac"] / roof_valu["formulation_ceiling_frac"]
+    ci = acs_clock_issue()
+    if ci is not None:
+        roof_valu["clock_ghz"] = ci["clock_ghz"]
+        roof_valu["issue_utilisation"] = ci["valu_issue_utilisation"]
+        roof_valu["frac_at_clock"] = roof_valu["frac"] * 2.4 / ci["clock_ghz"]
+        roof_valu["clock_source"] = ci["source"]
     if tm_alone.get(acs_stage):
         roof_valu["ms_per_launch"] = acs_ms
         roof_valu["ms_per_launch_alone"] = tm_alone[acs_stage]
@@ -651,11 +692,11 @@ def main():
     roof_hbm = {"kernel": f"{demod_kernel[5:]} (findIndex + FFT + DQPSK)", "bound": "hbm",
                 "achieved": demod_bytes / (demod_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "traffic": pmc_traffic(demod_kernel, args.workload), "algorithmic_bytes": demod_bytes,
-                "note": "algorithmic bytes: 8*T_s cf32 in + 2K soft bits out as RING8 bytes (ibits + 127; "
-                        "SURVEY 8(d)'s 26,560 B/symbol assumes int16 out) per data symbol + 8*T_u of the "
-                        "findIndex window per frame.  ms_per_launch is the launch's span on its stream: the "
-                        "demod is queued once run r-2's ACS is done, so its span includes the time its "
-                        "workgroups wait for the slots the running ACS still holds; frac_alone is the "
+                "note": f"algorithmic bytes: {bps}*T_s of {args.iq_format} samples in + 2K soft bits out as RING8 "
+                        "bytes (ibits + 127) per data symbol + the findIndex window's T_u samples per frame "
+                        "(SURVEY 8(d)'s 26,560 B/symbol counts cf32 in, int16 out).  ms_per_launch is the launch's "
+                        "span on its stream: the demod is queued once run r-2's ACS is done, so its span includes "
+                        "the time its workgroups wait for the slots the running ACS still holds; frac_alone is the "
                         "kernel's own rate"}
     roof_hbm["frac"] = roof_hbm["achieved"] / roof_hbm["peak"]
     if tm_alone.get("demod"):
@@ -669,11 +710,11 @@ def main():
         "value": value, "unit": "symbols/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": el / args.steps * 1e3, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32 (OFDM) + u8 soft bits (ring) + u16x2 packed path metrics (Viterbi, exact)",
-        "data": f"synthetic (dabsynth transmitter, 30 dB SNR, CFO {args.cfo:g} Hz)"
-                + (", int16 .sdr samples scattered from rank 0 over RCCL" if rccl else ""),
+        "data": f"synthetic (dabsynth transmitter, 30 dB SNR, CFO {args.cfo:g} Hz, amplitude {AMPLITUDE}), "
+                f"stored as {FORMAT_DESC[args.iq_format]}",
         "config": {"workload": wl_desc, "ensembles_per_gpu": E, "frames_per_step": F,
-                   "parallelism": f"ensemble-shard x{world}", "iq_source": "rccl-scatter" if rccl else "rank-local",
-                   "cfo_hz": args.cfo, "msc_output": args.msc_format},
+                   "parallelism": f"ensemble-shard x{world}", "iq_source": "rank-local",
+                   "iq_format": args.iq_format, "cfo_hz": args.cfo, "msc_output": args.msc_format},
         "realtime_ensembles_per_gpu": value / world / RT_SYMBOLS,
         "roofline": roofline,
         "roofline_hbm_demod": roof_hbm,
@@ -688,32 +729,33 @@ def main():
         # the whole step priced at the front end's algorithmic bytes
         "hbm_frac_step": value / world * SYMBOL_BYTES / (HBM_PEAK_GBS * 1e9),
         "hbm_frac_step_note": "BASELINE.md 4.4's definition: symbols/s per GPU x 26,560 B (8 T_s cf32 in + 2 x 3072 "
-                              "int16 out per symbol) / 8 TB/s (the ring now holds the soft bits as bytes: 23,488 B "
-                              "per symbol move)",
+                              "int16 out per symbol) / 8 TB/s; the bytes the front end moves per symbol here: "
+                              f"{bps} T_s in + 3072 out = {bps * TS + 3072} B",
     }
     if delivered is not None:
         out["delivered_symbols_per_s"] = delivered.pop("value")
         out["delivered"] = delivered
     if sync_loss is not None:
         out["sync_loss"] = sync_loss
-    if probe is not None:
-        out["stream_split"] = probe
-    if rccl:
-        out["stream_split"] = {"mode": "fed end to end: rank 0 -> every rank, grouped send/recv per step chunk",
-                               "backend": dist.get_backend(), "distinct_ensembles": world * E,
-                               "bytes_per_rank_per_step": E * 2 * cs * 2}
+    if c4 is not None:
+        out["c4_fed"] = c4
     if cpu is not None:
         t = cpu["tot"]
         out["cpu_baseline"] = {
             "value": cpu["value"], "unit": "symbols/s", "cores": cpu["cores"], "kind": cpu["kind"],
-            "sample": f"{cpu['cores']} workers pinned one per core (of nproc {cpu['nproc']}, {cpu['cpu']}), each "
-                      f"its own synthetic {args.workload.upper()} ensemble (24 frames per pass incl. the AFC's "
-                      f"convergence, {len(SUBCH)} subch) for "
-                      f"~{args.cpu_seconds:.0f}s: {t['symbols']} symbols.  FIC/MSC Viterbi + depuncture = reference "
-                      "viterbi.cpp+spiral-sse.c+deconvolve.cpp, DAB+ = reference reed-solomon.cpp+"
-                      "firecode-checker.cpp (compiled from /root/reference in oracle/_ref); OFDM = the oracle's C "
-                      "restatement of ofdm-processor.cpp/ofdm-decoder.cpp/phasereference.cpp with a double-"
-                      "precision radix-2 FFT (FFTW3f and Qt absent): kind 'port'",
+            "affinity_cores": cpu["affinity"], "omp_num_threads": cpu["omp"],
+            "fft": "fp32 radix-4 Stockham (oracle orc_fft2048_f32, FFTW3f's precision class; FFTW3f absent)",
+            "cpu_quota_cores": cpu["quota"],
+            "sample": f"{cpu['cores']} workers pinned one per core (affinity lists {cpu['affinity']} of nproc "
+                      f"{cpu['nproc']}, {cpu['cpu']}; the box's CPU share: OMP_NUM_THREADS {cpu['omp']}, cgroup "
+                      f"quota {cpu['quota']} cores), each its own synthetic "
+                      f"{args.workload.upper()} ensemble (24 frames per pass incl. the AFC's convergence, "
+                      f"{len(SUBCH)} subch) for ~{args.cpu_seconds:.0f}s: {t['symbols']} symbols.  FIC/MSC Viterbi "
+                      "+ depuncture = reference viterbi.cpp+spiral-sse.c+deconvolve.cpp, DAB+ = reference "
+                      "reed-solomon.cpp+firecode-checker.cpp (compiled from /root/reference in oracle/_ref); OFDM = "
+                      "the oracle's C restatement of ofdm-processor.cpp/ofdm-decoder.cpp/phasereference.cpp with "
+                      "the reference's 2.048 M-entry oscillatorTable and an fp32 radix-4 FFT standing in for "
+                      "FFTW3f (FFTW3f and Qt absent): kind 'port'",
             "stages_cpu_seconds": {"ofdm": t["t_ofdm"], "fic": t["t_fic"], "msc": t["t_msc"],
                                    "dabplus": t["t_dabplus"]},
             "decoded_mbit_per_s": (t["fic_bits"] + t["msc_bits"]) / cpu["secs"] / 1e6,
@@ -721,6 +763,94 @@ def main():
             "realtime_ensembles": cpu["value"] / RT_SYMBOLS,
         }
     print(json.dumps(out))
+
+
+def c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs, fed_ph, fmt, steps,
+               truth, seed0, msc_format, warmup=2):
+    """BASELINE configs[3] end to end: every rank decodes its E ensembles from samples rank
+    0 sends it over RCCL (FedSplit: chunk k + 2 of every stream travels while step k
+    decodes; the ranks' chunk phases reach rank 0 once, untimed -- rank 0 holds the
+    recordings).  Each rank's stream buffer is a torch tensor the pipeline reads in place
+    (dabgpu_pipe_set_iq_format).  Fails soft: an error on any rank before the timed
+    steps is agreed on by all ranks and reported instead of a rate."""
+    import torch
+    fcode, bps, dt = FORMATS[fmt]
+    err = None
+    nch = warmup + steps + 4                             # + the checked step, the acquisition, 2 ahead
+    stride_f = nch * cs
+    try:
+        dev = torch.device(f"cuda:{rank_device(local)}") if torch.cuda.is_available() else torch.device("cpu")
+        mine = torch.from_numpy(fed_ph).to(dev)
+        tdt = {np.uint8: torch.uint8, np.int16: torch.int16}[dt]
+        fiq = torch.zeros((E, 2 * stride_f), dtype=tdt, device=dev)
+    except Exception as e:                              # noqa: BLE001 -- reported in the line
+        err = repr(e)[:300]
+    if allreduce_max(dist, 1.0 if err else 0.0) > 0:
+        return {"error": err or "another rank failed its setup"}
+    src = gather_to_rank0(dist, rank, world, mine)      # setup: rank 0 now holds every rank's streams
+    phases = fed_ph.shape[0]
+    split = FedSplit(dist, rank, world, E, phases, src=src,
+                     dst=lambda e, k: fiq[e, 2 * k * cs:2 * (k + 1) * cs])
+    if rank == 0:                                       # rank 0 reads its own recordings in place
+        for k in range(nch):
+            fiq[:, 2 * k * cs:2 * (k + 1) * cs].copy_(src[0][k % phases])
+    got = [nch if rank == 0 else 0]
+
+    def feed(k):                                        # chunk k: begin ... end
+        if k < nch:
+            reqs = split.begin(k)
+            return lambda: (split.end(reqs), got.__setitem__(0, max(got[0], k + 1)))
+        return lambda: None
+    for k in range(2):
+        feed(k)()
+    pipe = dabamd.Pipeline(ctx, E, F, subs)
+    pipe.set_iq_format(fcode)
+    if msc_format == "packed":
+        pipe.set_packed(True)
+    buf = _TorchBuf(fiq)
+
+    def avail():
+        return [min(stride_f, got[0] * cs)] * E
+
+    def step(k, download=False):
+        done = feed(k + 2)                               # chunk k + 2 travels while step k decodes
+        r = pipe.run(buf, stride_f, avail(), download=download)
+        if dabplus:
+            pipe.dabplus(download=download)
+        done()
+        return r
+    pipe.acquire(buf, stride_f, [0] * E, avail())
+    for i in range(warmup):
+        step(i)
+    pipe.sync()
+    barrier(dist)
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(warmup + i)
+    pipe.sync()
+    el = time.perf_counter() - t0
+    barrier(dist)
+    el = allreduce_max(dist, el)
+    st0 = pipe.state(0)
+    fic, crc, msc, valid = step(warmup + steps, download=True)
+    if pipe.packed:
+        msc = np.unpackbits(msc, axis=-1)
+    check = check_step(truth, P, st0, pipe.state(0), fic, crc, msc, valid, SUBCH)
+    check["rank"] = rank
+    check["seed"] = seed0
+    checks = gather_objects(dist, check)
+    pipe.close()
+    nbytes = E * cs * bps
+    ms = el / steps * 1e3
+    return {"value": world * E * F * 76 * steps / el, "unit": "symbols/s", "ms_per_step": ms, "steps": steps,
+            "ensembles": world * E, "format": FORMAT_DESC[fmt], "backend": dist.get_backend(),
+            "bytes_per_rank_per_step": nbytes, "GBps_per_destination": nbytes / (ms * 1e-3) / 1e9,
+            "GBps_out_of_rank0": (world - 1) * nbytes / (ms * 1e-3) / 1e9,
+            "checked_steps": checks,
+            "note": "rank 0 holds every rank's recorded streams and sends each rank chunk k + 2 of ITS ensembles "
+                    "(E grouped sends per destination: a scatter, each destination over its own xGMI link) while "
+                    "step k decodes; the receivers' pipelines read the samples in place (u8/s16 converted in the "
+                    "kernels' loads).  Link-bound by design: DESIGN.md section 7"}
 
 
 def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist, truth, P):
@@ -786,7 +916,7 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
                       "(dabgpu_pipe_fetch), overlapping the next run"}
 
 
-def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, base_ms):
+def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, base_ms, fmt="f32"):
     """The price of a sync loss (ofdm-processor.cpp:354-357: findIndex fails -> notSynced,
     the null search from where the stream is).  Before step k0 + 2j + 1 of each mode, stream
     j gets an interferer over 300,000 samples (1.5 frames) in the middle of that step's
@@ -799,8 +929,10 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
     rng = np.random.default_rng(11)
     ph = 2 * np.pi * 100e3 / 2048000 * np.arange(n)
     jam = np.empty((n, 2), np.float32)
-    jam[:, 0] = np.cos(ph) + rng.normal(0, 0.1, n)
-    jam[:, 1] = np.sin(ph) + rng.normal(0, 0.1, n)
+    jam[:, 0] = AMPLITUDE * (np.cos(ph) + rng.normal(0, 0.1, n))
+    jam[:, 1] = AMPLITUDE * (np.sin(ph) + rng.normal(0, 0.1, n))
+    jam = to_raw(jam.reshape(-1), fmt)
+    bps = FORMATS[fmt][1]
     res = {}
     j = 0
     for mode in ("sync", "async"):
@@ -816,7 +948,7 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
             s = j % E
             at = pos0[s] + (i + 1) * F * TF + F // 2 * TF + 40000
             if at + n < stride:
-                diq.upload_at(jam.reshape(-1), (s * 2 * stride + 2 * at) * 4)
+                diq.upload_at(jam, (s * stride + at) * bps)
                 losses += 1
             j += 1
         pipe.sync()
@@ -860,36 +992,6 @@ class _TorchBuf:
     def __init__(self, t):
         import ctypes as C
         self.ptr = C.c_void_p(t.data_ptr())
-
-
-def stream_split_probe(dist, rank, world, local, E, F, reps=3):
-    """Time the C4 stream split on its own: rank 0 sends one step's int16 IQ chunk
-    (E streams x F frames, 4 B per sample) to every other rank in one grouped
-    send/recv; link-bound symbols/s = what the ranks could decode if fed this way."""
-    import torch
-    if dist.get_backend() != "nccl":
-        return None
-    dev = f"cuda:{rank_device(local)}"
-    cs = F * TF
-    buf = torch.ones((E, 2 * cs), dtype=torch.int16, device=dev)
-    ts = []
-    for i in range(reps + 1):
-        dist.barrier()
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for r in scatter_chunk(dist, rank, world, [buf] * world if rank == 0 else None, buf):
-            r.wait()
-        torch.cuda.synchronize()
-        dist.barrier()
-        if i:
-            ts.append(allreduce_max(dist, time.perf_counter() - t0))
-    t = min(ts)
-    nbytes = buf.numel() * 2
-    return {"bytes_per_rank_per_step": nbytes, "seconds_per_step": t,
-            "GBps_out_of_rank0": (world - 1) * nbytes / t / 1e9, "GBps_per_destination": nbytes / t / 1e9,
-            "link_bound_symbols_per_s": world * E * F * 76 / t,
-            "note": "one step's int16 IQ for every rank from rank 0, grouped send/recv over RCCL (xGMI); the "
-                    "decode is not overlapped here -- see --iq-source rccl for the fed end-to-end rate"}
 
 
 if __name__ == "__main__":

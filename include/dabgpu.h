@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DABGPU_ABI_VERSION 4
+#define DABGPU_ABI_VERSION 5
 
 /* error codes */
 #define DABGPU_OK          0
@@ -89,7 +89,7 @@ typedef struct {
  * (k = 1, 2, ...), localPhase = (lp - k*phase) mod 2048000 and the
  * sample is multiplied by oscillatorTable[localPhase]. */
 typedef struct {
-    int64_t iq_base;    /* element offset (cf32 units) of the stream in the IQ buffer */
+    int64_t iq_base;    /* sample offset of the stream in the IQ buffer */
     int64_t n_samples;  /* samples of this stream readable from iq_base (bounds check) */
     int64_t window;     /* first sample of the T_u sync window (SyncOnPhase) */
     int64_t block0;     /* first sample of block 0 = window + startIndex */
@@ -155,6 +155,7 @@ int         dabgpu_event_elapsed(dabgpu_ctx *ctx, int slot_a, int slot_b, float 
  *                  64-69, readBuffer) through libsndfile's sf_readf_float: x / 32768
  * n_pairs I/Q pairs: src_d holds 2*n_pairs values, iq_d receives 2*n_pairs floats.
  * Asynchronous on the context stream (dabgpu_sync to wait). */
+#define DABGPU_IQ_F32  0   /* interleaved cf32: what every entry point reads by default */
 #define DABGPU_IQ_U8   1
 #define DABGPU_IQ_S16  2
 int dabgpu_iq_convert(dabgpu_ctx *ctx, int format, const void *src_d, int64_t n_pairs, float *iq_d);
@@ -199,6 +200,13 @@ int dabgpu_ofdm_sync_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_fram
 /* The kernels' NCO: oscillatorTable[first .. first+n-1] as the front-end kernels
  * compute it (float2 into out_d) -- for checking it against the table exhaustively. */
 int dabgpu_nco_eval(dabgpu_ctx *ctx, int32_t first, int32_t n, float *out_d);
+/* Test hook of the fused demod's NCO (getSamples' v *= oscillatorTable[localPhase],
+ * ofdm-processor.cpp:76-81,202-226): dabgpu_ofdm_demod with `chunks` workgroups per
+ * frame (1: one recurrence over all 75 symbols, as the pipeline runs C3) that also writes
+ * every data symbol's mixed FFT input, mix_d[out_slot][75][2048] cf32 (the samples
+ * [T_g, T_s) of symbol l after the NCO), for comparison with the reference's table. */
+int dabgpu_ofdm_demod_mix(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n, int chunks,
+                          float *mix_d, int16_t *softbits_d);
 
 /* One symbol at a time (the reference's ofdmDecoder call pattern, ofdm-decoder.cpp:
  * 85-190), samples already mixed by the caller: kind 0 = block 0 (samples_d holds
@@ -295,10 +303,10 @@ int dabgpu_pipe_create(dabgpu_ctx *ctx, const dabgpu_pipe_cfg *cfg, dabgpu_pipe 
 int dabgpu_pipe_destroy(dabgpu_pipe *p);
 /* Acquire (notSynced/SyncOnNull/SyncOnEndNull, ofdm-processor.cpp:274-338)
  * every stream not yet synchronised from sample start_h[s] of its IQ (device,
- * stream s at iq_d + 2*stream_stride*s, n_avail_h[s] samples).  Optional:
+ * stream s at sample stream_stride*s of iq_d, n_avail_h[s] samples).  Optional:
  * dabgpu_pipe_run acquires unsynchronised streams itself, from their current
  * position (sample 0 for a new pipeline). */
-int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride,
+int dabgpu_pipe_acquire(dabgpu_pipe *p, const void *iq_d, int64_t stream_stride,
                         const int64_t *start_h, const int64_t *n_avail_h);
 /* Decode the next n_frames frames of every stream, as ofdmProcessor::run does:
  * a stream whose findIndex fails goes back to the null-symbol search from where it
@@ -313,7 +321,7 @@ int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride
  * Returns 0 when every stream decoded n_frames frames, DABGPU_E_STATE when one
  * ran out of samples (its decoded frames are still delivered; see
  * dabgpu_pipe_state). */
-int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq_d, int64_t stream_stride, const int64_t *n_avail_h,
+int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq_d, int64_t stream_stride, const int64_t *n_avail_h,
                     uint8_t *fic_bits_d, uint8_t *fic_crc_d, uint8_t *msc_bits_d, int32_t msc_stride,
                     uint8_t *msc_valid_h);
 /* DAB+ superframe layer for the CIFs of the last dabgpu_pipe_run (call once per
@@ -333,6 +341,15 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes_d, int32_t sf_stride, 
  * (dabgpu_pipe_fetch).  At most 512 frames per run. */
 #define DABGPU_SF_SLOTS(n_frames) ((4 * (n_frames) + 4) / 5 + 1)
 int dabgpu_pipe_set_dabplus_compact(dabgpu_pipe *p, int on);
+/* Sample format of the streams dabgpu_pipe_acquire / dabgpu_pipe_run read (default
+ * DABGPU_IQ_F32): DABGPU_IQ_S16 (interleaved int16, the .sdr recording's PCM16) or
+ * DABGPU_IQ_U8 (interleaved u8, the .raw recording / dabstick) are converted exactly
+ * in the kernels' sample loads, with the file readers' scaling (see dabgpu_iq_convert),
+ * so the decode equals that of the converted cf32 stream; the stream stride and
+ * n_avail stay in samples.  Takes effect at the next call. */
+int dabgpu_pipe_set_iq_format(dabgpu_pipe *p, int format);
+/* dabgpu_pipe_state takes a finished background null search's results first, so
+ * st->acquiring is 0 once the search no longer reads iq_d. */
 int dabgpu_pipe_state(dabgpu_pipe *p, int stream, dabgpu_stream_state *st);
 /* [n_streams][n_frames] records of the last dabgpu_pipe_run */
 int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info_h);
@@ -350,12 +367,15 @@ int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info_h);
  *                           found the null (its frames are the same, delivered later: it
  *                           decodes fewer than n_frames in the runs it misses, with
  *                           DABGPU_OK).  iq_d must stay valid until the search ends
- *                           (dabgpu_stream_state.acquiring).  dabgpu_pipe_sync does not wait
- *                           for a background search.
+ *                           (dabgpu_stream_state.acquiring, or dabgpu_pipe_acquire_wait).
+ *                           dabgpu_pipe_sync does not wait for a background search; the
+ *                           other control ops do (its result is applied first, so the
+ *                           control is the last word)
  *   DABGPU_CTL_ACQ_SYNC     (default) the run waits for the search and delivers n_frames
  *   DABGPU_CTL_INJECT_BOUNDS fault injection (stream ignored): the next run's MSC decoder
  *                           is handed a subchannel offset past the soft-bit ring; its
- *                           kernels refuse it (zeros read instead), and dabgpu_pipe_sync or
+ *                           kernels refuse it (erasures read instead: the depunctured
+ *                           value 0, RING8 byte 127), and dabgpu_pipe_sync or
  *                           the next run reports DABGPU_E_BOUNDS once -- the error path of
  *                           the back-end streams, for tests */
 #define DABGPU_CTL_RESET      1
@@ -374,6 +394,9 @@ int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op);
  * output buffers other than run r's unless this was called in between.  Also
  * reports a kernel that refused out-of-bounds work (DABGPU_E_BOUNDS). */
 int dabgpu_pipe_sync(dabgpu_pipe *p);
+/* Wait for a background null search (DABGPU_CTL_ACQ_ASYNC) in flight and apply its
+ * result; afterwards no search reads iq_d.  0 when none is in flight. */
+int dabgpu_pipe_acquire_wait(dabgpu_pipe *p);
 /* per-stage kernel time (HIP events on each stage's stream, no synchronisation added):
  * dabgpu_pipe_set_profiling(p, 1) times the last dabgpu_pipe_run, (p, 2) every run
  * since the call (summed; launches counts them); 0 turns it off.  Mode 3 is mode 2
@@ -409,6 +432,9 @@ int dabgpu_pipe_frames(dabgpu_pipe *p, dabgpu_frame *frames_h, int32_t *start_in
  * Which frames the GUI is shown (every 8th) is the caller's choice, as in the
  * reference.  Costs 12 KB of HBM writes per frame while on. */
 int dabgpu_pipe_set_display(dabgpu_pipe *p, int on);
+/* The symbol (1..75) the display feed keeps, ofdmDecoder::set_displayToken (declared in
+ * ofdm-decoder.h:50, displayToken = 2 at ofdm-decoder.cpp:61); takes effect at the next run. */
+int dabgpu_pipe_set_display_token(dabgpu_pipe *p, int token);
 /* MSC output format of the following runs: on = 0 (default) one bit per byte, as
  * deconvolve delivers it (viterbi.cpp:240-241); on = 1 eight bits per byte, msb first
  * (the packing of mp4Processor::addtoFrame, mp4processor.cpp:115-121 -- numpy packbits

@@ -237,16 +237,192 @@ void orc_fft2048(const float *in, float *out, int inverse) {
     }
 }
 
+/* 2048-point FFT in fp32 (round 5): the precision class of the reference's FFTW3f
+ * (fft.cpp:31-121 links libfftw3f with FFTW_ESTIMATE plans; FFTW is an un-vendored
+ * dependency absent from this image).  A Stockham radix-4 transform --
+ * five radix-4 DIF passes (n = 2048, 512, 128, 32, 8) and one radix-2 pass, natural
+ * order in and out -- with every butterfly and twiddle product in float (two rounded
+ * products and a rounded sum per real part, no FMA) and the twiddles computed in
+ * double and rounded once, as FFTW precomputes its twiddles.  Forward unscaled;
+ * inverse = conj(FFT(conj(x))) x 1/N (fft.cpp:109-121).  Split re/im arrays so the
+ * passes vectorise.  Used (1) for the fp32 floor of the soft values
+ * (tests/test_gpu_parity.py, test_demod_nco_matches_oracle) and (2) as the CPU
+ * baseline's FFT (bench.py cpu_baseline). */
+static float g_w32r[ORC_TU], g_w32i[ORC_TU];
+static void w32_init(void) {
+    static int init = 0;
+    if (init) return;
+    for (int k = 0; k < ORC_TU; k++) {
+        g_w32r[k] = (float)cos(2.0 * M_PI * k / ORC_TU);
+        g_w32i[k] = (float)-sin(2.0 * M_PI * k / ORC_TU);
+    }
+    init = 1;
+}
+/* one radix-4 DIF pass of the Stockham transform: sequences of length n = 4m at
+ * stride s (x) -> y */
+__attribute__((optimize("O3", "tree-vectorize")))
+static void r4pass(const float *restrict xr, const float *restrict xi, float *restrict yr, float *restrict yi,
+                   int m, int s) {
+    for (int p = 0; p < m; p++) {
+        const float w1r = g_w32r[p * s], w1i = g_w32i[p * s];
+        const float w2r = g_w32r[2 * p * s], w2i = g_w32i[2 * p * s];
+        const float w3r = g_w32r[3 * p * s], w3i = g_w32i[3 * p * s];
+        const float *ar = xr + s * p, *ai = xi + s * p;
+        float *or_ = yr + s * 4 * p, *oi = yi + s * 4 * p;
+        for (int q = 0; q < s; q++) {
+            const float a_r = ar[q], a_i = ai[q];
+            const float b_r = ar[q + s * m], b_i = ai[q + s * m];
+            const float c_r = ar[q + 2 * s * m], c_i = ai[q + 2 * s * m];
+            const float d_r = ar[q + 3 * s * m], d_i = ai[q + 3 * s * m];
+            const float apc_r = a_r + c_r, apc_i = a_i + c_i;
+            const float amc_r = a_r - c_r, amc_i = a_i - c_i;
+            const float bpd_r = b_r + d_r, bpd_i = b_i + d_i;
+            const float jbmd_r = -(b_i - d_i), jbmd_i = b_r - d_r;      /* j (b - d) */
+            or_[q] = apc_r + bpd_r; oi[q] = apc_i + bpd_i;
+            const float t1r = amc_r - jbmd_r, t1i = amc_i - jbmd_i;
+            const float t2r = apc_r - bpd_r, t2i = apc_i - bpd_i;
+            const float t3r = amc_r + jbmd_r, t3i = amc_i + jbmd_i;
+            /* two rounded products and one rounded sum per part (no FMA: -ffp-contract=off) */
+            or_[q + s] = w1r * t1r - w1i * t1i; oi[q + s] = w1r * t1i + w1i * t1r;
+            or_[q + 2 * s] = w2r * t2r - w2i * t2i; oi[q + 2 * s] = w2r * t2i + w2i * t2r;
+            or_[q + 3 * s] = w3r * t3r - w3i * t3i; oi[q + 3 * s] = w3r * t3i + w3i * t3r;
+        }
+    }
+}
+/* the first pass (s = 1), vectorised over p: the same butterflies */
+__attribute__((optimize("O3", "tree-vectorize")))
+static void r4pass_first(const float *restrict xr, const float *restrict xi, float *restrict yr, float *restrict yi) {
+    const int m = ORC_TU / 4;
+    for (int p = 0; p < m; p++) {
+        const float w1r = g_w32r[p], w1i = g_w32i[p], w2r = g_w32r[2 * p], w2i = g_w32i[2 * p];
+        const float w3r = g_w32r[3 * p], w3i = g_w32i[3 * p];
+        const float a_r = xr[p], a_i = xi[p], b_r = xr[p + m], b_i = xi[p + m];
+        const float c_r = xr[p + 2 * m], c_i = xi[p + 2 * m], d_r = xr[p + 3 * m], d_i = xi[p + 3 * m];
+        const float apc_r = a_r + c_r, apc_i = a_i + c_i;
+        const float amc_r = a_r - c_r, amc_i = a_i - c_i;
+        const float bpd_r = b_r + d_r, bpd_i = b_i + d_i;
+        const float jbmd_r = -(b_i - d_i), jbmd_i = b_r - d_r;
+        const float t1r = amc_r - jbmd_r, t1i = amc_i - jbmd_i;
+        const float t2r = apc_r - bpd_r, t2i = apc_i - bpd_i;
+        const float t3r = amc_r + jbmd_r, t3i = amc_i + jbmd_i;
+        yr[4 * p] = apc_r + bpd_r; yi[4 * p] = apc_i + bpd_i;
+        yr[4 * p + 1] = w1r * t1r - w1i * t1i; yi[4 * p + 1] = w1r * t1i + w1i * t1r;
+        yr[4 * p + 2] = w2r * t2r - w2i * t2i; yi[4 * p + 2] = w2r * t2i + w2i * t2r;
+        yr[4 * p + 3] = w3r * t3r - w3i * t3i; yi[4 * p + 3] = w3r * t3i + w3i * t3r;
+    }
+}
+__attribute__((optimize("O3", "tree-vectorize")))
+static void r2pass_last(const float *restrict xr, const float *restrict xi, float *restrict yr, float *restrict yi) {
+    const int s = ORC_TU / 2;
+    for (int q = 0; q < s; q++) {
+        const float a_r = xr[q], a_i = xi[q], b_r = xr[q + s], b_i = xi[q + s];
+        yr[q] = a_r + b_r; yi[q] = a_i + b_i;
+        yr[q + s] = a_r - b_r; yi[q + s] = a_i - b_i;
+    }
+}
+/* x -> y (pass 1), y -> x, x -> y, y -> x, x -> y (n = 8), y -> x (radix-2): result in x */
+static void fft2048_f32_fwd(float *xr, float *xi, float *yr, float *yi) {
+    r4pass_first(xr, xi, yr, yi);
+    r4pass(yr, yi, xr, xi, 128, 4);
+    r4pass(xr, xi, yr, yi, 32, 16);
+    r4pass(yr, yi, xr, xi, 8, 64);
+    r4pass(xr, xi, yr, yi, 2, 256);
+    r2pass_last(yr, yi, xr, xi);
+}
+void orc_fft2048_f32(const float *in, float *out, int inverse) {
+    w32_init();
+    float xr[ORC_TU], xi[ORC_TU], yr[ORC_TU], yi[ORC_TU];
+    const float sg = inverse ? -1.0f : 1.0f;          /* inverse: conj in, conj out */
+    for (int k = 0; k < ORC_TU; k++) { xr[k] = in[2 * k]; xi[k] = sg * in[2 * k + 1]; }
+    fft2048_f32_fwd(xr, xi, yr, yi);          /* 5 radix-4 passes + the radix-2 pass end in xr/xi */
+    const float factor = (float)(1.0 / (float)ORC_TU);
+    for (int k = 0; k < ORC_TU; k++) {
+        float fr = xr[k], fi = sg * xi[k];
+        if (inverse) { fr *= factor; fi *= factor; }
+        out[2 * k] = fr; out[2 * k + 1] = fi;
+    }
+}
+
+/* two more fp32 transforms of FFTW3f's precision class, for the spread of fp32 FFT
+ * rounding (the soft values' fp32 floor, tests/test_gpu_parity.py): the radix-2
+ * decimation-in-time transform of orc_fft2048 carried out in float (bit-reversed load),
+ * and the radix-2 decimation-in-frequency (Gentleman-Sande) transform (bit-reversed
+ * store); float butterflies, twiddles rounded once from double, no FMA */
+static void fft2048_f32_r2(const float *in, float *out, int inverse, int dif) {
+    w32_init();
+    float re[ORC_TU], im[ORC_TU];
+    const float sg = inverse ? -1.0f : 1.0f;
+    for (int n = 0; n < ORC_TU; n++) {
+        int r = n;
+        if (!dif) { r = 0; int x = n; for (int b = 0; b < 11; b++) { r = (r << 1) | (x & 1); x >>= 1; } }
+        re[r] = in[2 * n]; im[r] = sg * in[2 * n + 1];
+    }
+    if (!dif) {
+        for (int len = 2; len <= ORC_TU; len <<= 1) {
+            const int half = len >> 1, step = ORC_TU / len;
+            for (int s0 = 0; s0 < ORC_TU; s0 += len)
+                for (int j = 0; j < half; j++) {
+                    const float wr = g_w32r[j * step], wi = g_w32i[j * step];
+                    const float xr = re[s0 + j + half], xi = im[s0 + j + half];
+                    const float tr = xr * wr - xi * wi, ti = xr * wi + xi * wr;
+                    re[s0 + j + half] = re[s0 + j] - tr; im[s0 + j + half] = im[s0 + j] - ti;
+                    re[s0 + j] += tr; im[s0 + j] += ti;
+                }
+        }
+    } else {
+        for (int len = ORC_TU; len >= 2; len >>= 1) {
+            const int half = len >> 1, step = ORC_TU / len;
+            for (int s0 = 0; s0 < ORC_TU; s0 += len)
+                for (int j = 0; j < half; j++) {
+                    const float wr = g_w32r[j * step], wi = g_w32i[j * step];
+                    const float ar = re[s0 + j], ai = im[s0 + j], br = re[s0 + j + half], bi = im[s0 + j + half];
+                    re[s0 + j] = ar + br; im[s0 + j] = ai + bi;
+                    const float dr = ar - br, di = ai - bi;
+                    re[s0 + j + half] = dr * wr - di * wi; im[s0 + j + half] = dr * wi + di * wr;
+                }
+        }
+    }
+    const float factor = (float)(1.0 / (float)ORC_TU);
+    for (int k = 0; k < ORC_TU; k++) {
+        int r = k;
+        if (dif) { r = 0; int x = k; for (int b = 0; b < 11; b++) { r = (r << 1) | (x & 1); x >>= 1; } }
+        float fr = re[r], fi = sg * im[r];
+        if (inverse) { fr *= factor; fi *= factor; }
+        out[2 * k] = fr; out[2 * k + 1] = fi;
+    }
+}
+static void fft2048_f32_dit(const float *in, float *out, int inverse) { fft2048_f32_r2(in, out, inverse, 0); }
+static void fft2048_f32_dif(const float *in, float *out, int inverse) { fft2048_f32_r2(in, out, inverse, 1); }
+void orc_fft2048_kind(const float *in, float *out, int inverse, int kind) {
+    if (kind == 2) fft2048_f32_dit(in, out, inverse);
+    else if (kind == 3) fft2048_f32_dif(in, out, inverse);
+    else if (kind == 1) orc_fft2048_f32(in, out, inverse);
+    else orc_fft2048(in, out, inverse);
+}
+
+/* the front end's FFT: 0 = the double-precision "ideal" transform (the parity
+ * oracle), 1 = the fp32 radix-4 (FFTW3f's precision class, CPU baseline), 2 / 3 = the
+ * fp32 radix-2 DIT / DIF */
+typedef void (*orc_fft_fn)(const float *, float *, int);
+static orc_fft_fn fft_of(int kind) {
+    return kind == 1 ? orc_fft2048_f32 : kind == 2 ? fft2048_f32_dit : kind == 3 ? fft2048_f32_dif : orc_fft2048;
+}
+
 /* ------------------------------------------------------------ OFDM front */
 
 static float g_ref[2 * ORC_TU];
 static int16_t g_perm[ORC_K];
 static float g_refarg[18];
 static int g_tables = 0;
+/* oscillatorTable (ofdm-processor.cpp:76-81): 2,048,000 cf32, as the reference keeps it */
+static float *g_osc = NULL;
 static void tables_init(void) {
     if (g_tables) return;
     orc_ref_table(g_ref);
     orc_mapper(g_perm);
+    float *osc = (float *)malloc(sizeof(float) * 2 * ORC_INPUT_RATE);
+    for (int32_t i = 0; i < ORC_INPUT_RATE; i++) orc_osc_entry(i, &osc[2 * i], &osc[2 * i + 1]);
+    g_osc = osc;
     for (int i = 0; i < 18; i++) {           /* ofdm-decoder.cpp:71-74 */
         cf a = {g_ref[2 * ((ORC_TU + i) % ORC_TU)], g_ref[2 * ((ORC_TU + i) % ORC_TU) + 1]};
         cf b = {g_ref[2 * ((ORC_TU + i + 1) % ORC_TU)], g_ref[2 * ((ORC_TU + i + 1) % ORC_TU) + 1]};
@@ -255,16 +431,16 @@ static void tables_init(void) {
     g_tables = 1;
 }
 
-int32_t orc_find_index(const float *v, int16_t level, float *maxv, float *sumv) {   /* phasereference.cpp:60-88 */
+static int32_t find_index_(const float *v, int16_t level, float *maxv, float *sumv, orc_fft_fn fft) {
     tables_init();
     float X[2 * ORC_TU], R[2 * ORC_TU];
-    orc_fft2048(v, X, 0);
+    fft(v, X, 0);
     for (int i = 0; i < ORC_TU; i++) {
         cf a = {X[2 * i], X[2 * i + 1]}, b = {g_ref[2 * i], g_ref[2 * i + 1]};
         cf r = cmul_conjf(a, b);
         R[2 * i] = r.re; R[2 * i + 1] = r.im;
     }
-    orc_fft2048(R, X, 1);
+    fft(R, X, 1);
     float sum = 0;
     for (int i = 0; i < ORC_TU; i++) { cf z = {X[2 * i], X[2 * i + 1]}; sum += cabs_f(z); }
     float Max = -10000;
@@ -278,6 +454,9 @@ int32_t orc_find_index(const float *v, int16_t level, float *maxv, float *sumv) 
     if (Max < (float)level * sum / (float)ORC_TU)
         return (int32_t)(-fabsf(Max / (sum / (float)ORC_TU)) - 1);
     return maxIndex;
+}
+int32_t orc_find_index(const float *v, int16_t level, float *maxv, float *sumv) {   /* phasereference.cpp:60-88 */
+    return find_index_(v, level, maxv, sumv, orc_fft2048);
 }
 
 static int16_t get_middle(const float *X) {  /* ofdm-decoder.cpp:233-258 (incl. its "sum = oldMax") */
@@ -312,10 +491,10 @@ static inline float arg_pair(const float *X, int a, int b) {
     return carg_f(cmul_conjf(x, y));
 }
 
-int16_t orc_process_block0(const float *v, float *phase_ref, int flag, int method) {   /* ofdm-decoder.cpp:85-162 */
+static int16_t process_block0_(const float *v, float *phase_ref, int flag, int method, orc_fft_fn fft) {
     tables_init();
     float X[2 * ORC_TU];
-    orc_fft2048(v, X, 0);
+    fft(v, X, 0);
     if (phase_ref) memcpy(phase_ref, X, sizeof X);
     if (!flag) return 0;
     if (method == 0) return get_middle(X);
@@ -351,9 +530,12 @@ int16_t orc_process_block0(const float *v, float *phase_ref, int flag, int metho
     }
     return (int16_t)(index_1 - ORC_TU);
 }
+int16_t orc_process_block0(const float *v, float *phase_ref, int flag, int method) {   /* ofdm-decoder.cpp:85-162 */
+    return process_block0_(v, phase_ref, flag, method, orc_fft2048);
+}
 
-static void process_token_(const float *v, float *phase_ref, int16_t *ibits, float *softf, float *X) {
-    orc_fft2048(v + 2 * ORC_TG, X, 0);
+static void process_token_(const float *v, float *phase_ref, int16_t *ibits, float *softf, float *X, orc_fft_fn fft) {
+    fft(v + 2 * ORC_TG, X, 0);
     for (int i = 0; i < ORC_K; i++) {
         int index = g_perm[i];
         if (index < 0) index += ORC_TU;
@@ -370,7 +552,15 @@ static void process_token_(const float *v, float *phase_ref, int16_t *ibits, flo
 void orc_process_token(const float *v, float *phase_ref, int16_t *ibits, float *softf) {   /* ofdm-decoder.cpp:167-190 */
     tables_init();
     float X[2 * ORC_TU];
-    process_token_(v, phase_ref, ibits, softf, X);
+    process_token_(v, phase_ref, ibits, softf, X, orc_fft2048);
+}
+void orc_process_token_fft(const float *v, float *phase_ref, int16_t *ibits, float *softf, int fft_kind) {
+    tables_init();
+    float X[2 * ORC_TU];
+    process_token_(v, phase_ref, ibits, softf, X, fft_of(fft_kind));
+}
+int16_t orc_process_block0_fft(const float *v, float *phase_ref, int flag, int method, int fft_kind) {
+    return process_block0_(v, phase_ref, flag, method, fft_of(fft_kind));
 }
 
 void orc_freqcorr(const float *v, double *acc_re, double *acc_im, float *facc) {   /* ofdm-processor.cpp:424-425 */
@@ -386,7 +576,6 @@ void orc_freqcorr(const float *v, double *acc_re, double *acc_im, float *facc) {
 typedef struct {
     const float *iq; int64_t n, pos;
     int32_t localPhase; float sLevel;
-    float osc_cache_re, osc_cache_im; int32_t osc_cache_i;
     /* the spectrum feed (HAVE_SPECTRUM, ofdm-processor.cpp:161-180,220-238): sampleCnt
      * counts the samples of every getSample / getSamples call; at the end of the call that
      * takes it past INPUT_RATE / 7 the first 32768 raw samples read since the previous
@@ -411,11 +600,7 @@ static int get_sample_(orc_src *s, int32_t phase, cf *out) {
     s->pos++;
     s->localPhase -= phase;
     s->localPhase = (s->localPhase + ORC_INPUT_RATE) % ORC_INPUT_RATE;
-    if (s->osc_cache_i != s->localPhase) {
-        orc_osc_entry(s->localPhase, &s->osc_cache_re, &s->osc_cache_im);
-        s->osc_cache_i = s->localPhase;
-    }
-    cf o = {s->osc_cache_re, s->osc_cache_im};
+    cf o = {g_osc[2 * s->localPhase], g_osc[2 * s->localPhase + 1]};
     t = cmulf(t, o);
     s->sLevel = (float)(0.00001 * jan_abs(t) + (1 - 0.00001) * s->sLevel);
     *out = t;
@@ -441,7 +626,7 @@ static int get_samples(orc_src *s, cf *v, int n, int32_t phase) {  /* ofdm-proce
  * SyncOnPhase starts).  coarse + fine = 0. */
 int orc_null_scan(const float *iq, int64_t n, int scan, int32_t *attempts, int32_t *no_signal, int64_t *pos) {
     tables_init();
-    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0, 0, 0, NULL};
+    orc_src s = {iq, n, 0, 0, 0.0f, 0, 0, NULL};
     float *envBuffer = (float *)malloc(sizeof(float) * 32768);
     const int mask = 32768 - 1;
     int idx, ret = 0;
@@ -487,14 +672,24 @@ done:
 }
 
 static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
-                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf, orc_display *disp);
+                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf, orc_display *disp,
+                         int fftk);
 int orc_ofdm_run_display(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
                          orc_frame_info *info, int16_t *softbits, orc_display *disp) {
     /* per call (reentrant: tests run the oracle on several streams from threads) */
     float *envBuffer = (float *)malloc(sizeof(float) * 32768);
     cf *buf = (cf *)malloc(sizeof(cf) * ORC_L * ORC_TS);
     if (disp) { disp->n_disp = 0; disp->n_spec = 0; }
-    int ret = orc_ofdm_run_(iq, n, threshold, method, max_frames, info, softbits, envBuffer, buf, disp);
+    int ret = orc_ofdm_run_(iq, n, threshold, method, max_frames, info, softbits, envBuffer, buf, disp, 0);
+    free(envBuffer);
+    free(buf);
+    return ret;
+}
+int orc_ofdm_run_fft(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
+                     orc_frame_info *info, int16_t *softbits, int fft_kind) {
+    float *envBuffer = (float *)malloc(sizeof(float) * 32768);
+    cf *buf = (cf *)malloc(sizeof(cf) * ORC_L * ORC_TS);
+    int ret = orc_ofdm_run_(iq, n, threshold, method, max_frames, info, softbits, envBuffer, buf, NULL, fft_kind);
     free(envBuffer);
     free(buf);
     return ret;
@@ -505,9 +700,11 @@ int orc_ofdm_run(const float *iq, int64_t n, int16_t threshold, int method,
 }
 
 static int orc_ofdm_run_(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
-                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf, orc_display *disp) {
+                         orc_frame_info *info, int16_t *softbits, float *envBuffer, cf *buf, orc_display *disp,
+                         int fftk) {
     tables_init();
-    orc_src s = {iq, n, 0, 0, 0.0f, 1.0f, 0.0f, 0, 0, 0, disp};
+    orc_src s = {iq, n, 0, 0, 0.0f, 0, 0, disp};
+    orc_fft_fn fft = fft_of(fftk);
     int iq_cnt = 0;                      /* processToken's static cnt (ofdm-decoder.cpp:171) */
     const int mask = 32768 - 1;
     float phase_ref[2 * ORC_TU];
@@ -547,13 +744,13 @@ notSynced:
         int32_t lpw = s.localPhase;
         for (int i = 0; i < ORC_TU; i++)                  /* getSample, one at a time (:346-347) */
             if (!get_sample(&s, coarse + fine, &buf[i])) return frames;
-        int32_t startIndex = orc_find_index((const float *)buf, threshold, NULL, NULL);
+        int32_t startIndex = find_index_((const float *)buf, threshold, NULL, NULL, fft);
         if (startIndex < 0) goto notSynced;
         memmove(buf, &buf[startIndex], (size_t)(ORC_TU - startIndex) * sizeof(cf));
         int bidx = ORC_TU - startIndex;
         /* OFDM_PRS :383-406 */
         if (!get_samples(&s, &buf[bidx], ORC_TU - bidx, coarse + fine)) return frames;
-        int16_t correction = orc_process_block0((const float *)buf, phase_ref, f2, method);
+        int16_t correction = process_block0_((const float *)buf, phase_ref, f2, method, fft);
         if (f2) {
             if (correction == 0 && prev1 == 0 && prev2 == 0) f2 = 0;
             else if (correction != 100) {
@@ -571,7 +768,7 @@ notSynced:
             if (!get_samples(&s, buf, ORC_TS, coarse + fine)) return frames;
             orc_freqcorr((const float *)buf, NULL, NULL, fc);
             float X[2 * ORC_TU];
-            process_token_(( const float *)buf, phase_ref, ibits, NULL, X);
+            process_token_((const float *)buf, phase_ref, ibits, NULL, X, fft);
             if (dst) memcpy(dst + (l - 1) * 2 * ORC_K, ibits, sizeof ibits);
             /* the IQ display (ofdm-decoder.cpp:192-206): every 8th displayToken (2) the
              * carriers fft_buffer[0, K/2) and [T_u - 1 - K/2, T_u - 1) into iqBuffer */

@@ -13,7 +13,9 @@
  *   (2) the reference's intrinsic checks (FIB CRC, fire code, RS, AU CRC).
  * FFT parity is unpinned by construction: the reference links FFTW3f (an
  * un-vendored third-party dependency absent from this image); the oracle
- * uses a double-precision DFT rounded to float (an "ideal" fp32 FFT).
+ * uses a double-precision DFT rounded to float (an "ideal" fp32 FFT); an fp32
+ * radix-4 transform (orc_fft2048_f32, FFTW3f's precision class) measures the
+ * soft values' fp32 floor and serves the CPU baseline.
  */
 #ifndef DAB_ORACLE_H
 #define DAB_ORACLE_H
@@ -54,6 +56,13 @@ int16_t orc_process_block0(const float *v /*cf32[T_u]*/, float *phase_ref /*cf32
 int16_t orc_get_snr(const float *X /*cf32[T_u] spectrum*/);      /* ofdm-decoder.cpp:212-230 */
 void    orc_process_token(const float *v /*cf32[T_s]*/, float *phase_ref /*cf32[T_u] in/out*/,
                           int16_t *ibits /*[3072]*/, float *softf /*[3072] or NULL*/); /* ofdm-decoder.cpp:167-190 */
+/* the same with the fp32 radix-4 FFT (fft_kind 1: FFTW3f's precision class, the soft
+ * values' fp32 floor and the CPU baseline) or the double-precision one (0) */
+void    orc_fft2048_f32(const float *in /*cf32[2048]*/, float *out, int inverse);
+/* kind 0 double, 1 fp32 radix-4 Stockham, 2 fp32 radix-2 DIT, 3 fp32 radix-2 DIF */
+void    orc_fft2048_kind(const float *in, float *out, int inverse, int kind);
+void    orc_process_token_fft(const float *v, float *phase_ref, int16_t *ibits, float *softf, int fft_kind);
+int16_t orc_process_block0_fft(const float *v, float *phase_ref, int flag, int method, int fft_kind);
 void    orc_freqcorr(const float *v /*cf32[T_s]*/, double *acc_re, double *acc_im,
                      float *facc /*cf32 running, reference float order*/); /* ofdm-processor.cpp:424-425 */
 
@@ -75,6 +84,8 @@ typedef struct {
 int     orc_null_scan(const float *iq, int64_t n, int scan, int32_t *attempts, int32_t *no_signal, int64_t *pos);
 int     orc_ofdm_run(const float *iq /*cf32[n]*/, int64_t n, int16_t threshold, int method,
                      int max_frames, orc_frame_info *info, int16_t *softbits /*[max_frames][75][3072]*/);
+int     orc_ofdm_run_fft(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
+                         orc_frame_info *info, int16_t *softbits, int fft_kind);
 /* ... and the two display feeds of the reference's OFDM classes:
  *   iqBuffer (ofdmDecoder::processToken, ofdm-decoder.cpp:192-206): every 8th call with
  *     blkno == displayToken (2), fft_buffer[0, K/2) then [T_u-1-K/2, T_u-1): iq_disp[k]

@@ -51,6 +51,50 @@ __device__ __forceinline__ float2 nco_value(const double2 *tab, int32_t t) {
     const double2 v = nco_value_d(tab, t);
     return make_float2((float)v.x, (float)v.y);
 }
+// ---- recorded-IQ sample formats read by the front-end kernels (dabgpu.h DABGPU_IQ_*):
+// the conversion of the reference's file readers, exact in float, done in the load:
+//   F32  interleaved cf32 as virtualInput::getSamples hands it over
+//   S16  .sdr PCM16 (wavfiles.cpp:172, sf_readf_float: x / 32768)
+//   U8   .raw (rawfiles.cpp:115-117: float(x - 128) / 128.0 = x / 128 - 1)
+// raw: what a prefetch register holds (8, 4 or 2 bytes per sample); bps: bytes per sample
+template <int FMT> struct IqFmt;
+template <> struct IqFmt<DABGPU_IQ_F32> {
+    typedef float2 raw;
+    static constexpr int bps = 8;
+    __device__ static raw load(__amdgpu_buffer_rsrc_t r, int32_t off) {
+        return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
+    }
+    __device__ static float2 cvt(raw v) { return v; }
+};
+template <> struct IqFmt<DABGPU_IQ_S16> {
+    typedef uint32_t raw;
+    static constexpr int bps = 4;
+    __device__ static raw load(__amdgpu_buffer_rsrc_t r, int32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+    __device__ static float2 cvt(raw v) {
+        return make_float2((float)(int32_t)(int16_t)(v & 0xFFFFu) * 0x1p-15f, (float)((int32_t)v >> 16) * 0x1p-15f);
+    }
+};
+template <> struct IqFmt<DABGPU_IQ_U8> {
+    typedef uint32_t raw;
+    static constexpr int bps = 2;
+    __device__ static raw load(__amdgpu_buffer_rsrc_t r, int32_t off) { return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0); }
+    __device__ static float2 cvt(raw v) {
+        // (float)(x - 128) / 128 == x * 2^-7 - 1 exactly (x < 256): one fma per value
+        return make_float2(__builtin_fmaf((float)(v & 0xFFu), 0x1p-7f, -1.0f), __builtin_fmaf((float)((v >> 8) & 0xFFu), 0x1p-7f, -1.0f));
+    }
+};
+// sample i of a stream starting at `base` (plain loads, for the kernels that gather)
+template <int FMT>
+__device__ __forceinline__ float2 iq_at(const void *base, int64_t i) {
+    if constexpr (FMT == DABGPU_IQ_F32) return ((const float2 *)base)[i];
+    else if constexpr (FMT == DABGPU_IQ_S16) return IqFmt<FMT>::cvt(((const uint32_t *)base)[i]);
+    else return IqFmt<FMT>::cvt(((const uint16_t *)base)[i]);
+}
+template <int FMT>
+__device__ __forceinline__ const void *iq_stream(const void *iq, int64_t base) {
+    return (const char *)iq + base * IqFmt<FMT>::bps;
+}
+
 // FFT-internal product (fused is fine inside the transform)
 __device__ __forceinline__ float2 cmul(float2 a, float wr, float wi) {
     return make_float2(fmaf(a.x, wr, -a.y * wi), fmaf(a.x, wi, a.y * wr));

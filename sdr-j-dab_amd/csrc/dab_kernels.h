@@ -43,6 +43,10 @@ struct DemodAux {
                             // [T_u-1-K/2, T_u-1) -- the iqBuffer feed of processToken
                             // (ofdm-decoder.cpp:192-206)
     int32_t ring8;          // soft bits as RING8 bytes (the pipeline's ring), else int16
+    int32_t fmt;            // sample format of iq (DABGPU_IQ_F32 / S16 / U8)
+    int32_t disp_token;     // the symbol disp receives (ofdmDecoder's displayToken, 2 by default)
+    float2 *mix;            // test hook (dabgpu_ofdm_demod_mix): [out_slot][75][T_u] the NCO-mixed
+                            // FFT input of every data symbol, as the demod's FFT sees it
 };
 // The pipeline's soft-bit ring holds each ibits value v as the byte v + 127: processToken's
 // values are (int16_t)(q * 127.0) with |q| <= 1 (ofdm-decoder.cpp:188-189; a 0/0 gives 0),
@@ -172,13 +176,14 @@ struct DpJob {
     int32_t kmax;
 };
 
-hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+// iq: samples in format fmt (DABGPU_IQ_*); frame descriptors count samples
+hipError_t launch_prs_sync(hipStream_t st, const void *iq, int fmt, const dabgpu_frame *fr, int n, const OfdmTables &T,
                            int level, int32_t *si, float *mx, float *sm, bool general);
-hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+hipError_t launch_block0(hipStream_t st, const void *iq, int fmt, const dabgpu_frame *fr, int n, const OfdmTables &T,
                          int method, int16_t *corr, int16_t *snr, bool general);
 // aux.si non-null: every frame is placed by its own findIndex (block0 = window +
 // startIndex), reported through aux; else the descriptors' block0 / lp_data are used
-hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
+hipError_t launch_demod(hipStream_t st, const void *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
                         const DemodAux &aux);
 hipError_t launch_nco_eval(hipStream_t st, const OfdmTables &T, int32_t first, int32_t n, float2 *out);
@@ -189,7 +194,7 @@ hipError_t launch_take_error(hipStream_t st, int32_t *err, int32_t *h_err);
 hipError_t launch_front_publish(hipStream_t st, const float *part, int nchunks, int n, float *fc_d, float *h_fc,
                                 const int32_t *si_d, int32_t *h_si, const int16_t *snr_d, int16_t *h_snr,
                                 int32_t *err, int32_t *h_err);
-hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
+hipError_t launch_acquire(hipStream_t st, const void *iq, int fmt, const AcqJob *jobs, int n, const float2 *osc,
                           AcqResult *res);
 hipError_t launch_viterbi(hipStream_t st, const VitJob &job);
 hipError_t launch_acs(hipStream_t st, const VitJob &job);

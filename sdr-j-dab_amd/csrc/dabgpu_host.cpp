@@ -579,14 +579,14 @@ int dabgpu_event_elapsed(dabgpu_ctx *c, int a, int b, float *ms) {
 int dabgpu_prs_sync(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int16_t level, int32_t *si,
                     float *mx, float *sm) {
     if (!c || !iq || !fr || !si || n < 0) return fail(DABGPU_E_ARG, "bad args");
-    HIPCHK(launch_prs_sync(c->stream, iq, fr, n, c->T, level, si, mx, sm, true));
+    HIPCHK(launch_prs_sync(c->stream, iq, DABGPU_IQ_F32, fr, n, c->T, level, si, mx, sm, true));
     return 0;
 }
 int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int method, int16_t *corr,
                   int16_t *snr) {
     if (!c || !iq || !fr || !corr || n < 0) return fail(DABGPU_E_ARG, "bad args");
     if (method < 0 || method > 2) return fail(DABGPU_E_UNSUP, "freqSyncMethod %d", method);
-    HIPCHK(launch_block0(c->stream, iq, fr, n, c->T, method, corr, snr, true));
+    HIPCHK(launch_block0(c->stream, iq, DABGPU_IQ_F32, fr, n, c->T, method, corr, snr, true));
     return 0;
 }
 // symbols 1..75 of a frame are split over `chunks` workgroups of k_demod (each
@@ -642,6 +642,17 @@ int dabgpu_ofdm_symbol(dabgpu_ctx *c, const float *smp, int kind, float *spec, i
 int dabgpu_get_snr(dabgpu_ctx *c, const float *spectrum, int16_t *snr) {
     if (!c || !spectrum || !snr) return fail(DABGPU_E_ARG, "bad args");
     HIPCHK(launch_snr(c->stream, spectrum, snr));
+    return 0;
+}
+int dabgpu_ofdm_demod_mix(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int chunks, float *mix,
+                          int16_t *soft) {
+    if (!c || !iq || !fr || !mix || !soft || n < 0 || chunks < 1 || chunks > NSYM) return fail(DABGPU_E_ARG, "bad args");
+    void *part = nullptr;
+    int rc = scratch(c, SC_FC, sizeof(float2) * (size_t)n * chunks, &part);
+    if (rc) return rc;
+    DemodAux aux{};
+    aux.mix = (float2 *)mix;
+    HIPCHK(launch_demod(c->stream, iq, fr, n, chunks, c->T, soft, nullptr, (float *)part, true, aux));
     return 0;
 }
 int dabgpu_nco_eval(dabgpu_ctx *c, int32_t first, int32_t n, float *out) {
@@ -905,6 +916,8 @@ struct dabgpu_pipe {
     float2 *disp_d = nullptr;        // [S][R][K]
     bool display = false;
     bool packed = false;             // MSC output 8 bits per byte (dabgpu_pipe_set_packed)
+    int iq_fmt = DABGPU_IQ_F32;      // sample format of the streams (dabgpu_pipe_set_iq_format)
+    int disp_token = 2;              // the display feed's symbol (ofdm-decoder.cpp:61 displayToken)
     // background null search (DABGPU_CTL_ACQ_ASYNC): a stream that loses sync is searched
     // on its own low-priority stream while the others keep decoding; its results are
     // taken by the first dabgpu_pipe_run after they arrive
@@ -1196,7 +1209,7 @@ static int acq_apply(StreamSt &x, const AcqResult &r) {
 // its correctors: one k_acquire wave per stream.  A stream that finds the end of a
 // null symbol is synchronised at SyncOnPhase; one that runs out of samples stays
 // unsynchronised at the end of its samples (the next call continues from there).
-static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
+static int acquire_streams(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_t *n_avail,
                            const std::vector<int> &who, std::vector<StreamSt> &cur, int &found) {
     dabgpu_ctx *c = p->c;
     found = 0;
@@ -1208,7 +1221,7 @@ static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     if (rc) return rc;
     if ((rc = scratch(c, SC_ACQ, sizeof(AcqResult) * jobs.size(), &rd))) return rc;
     HIPCHK(hipMemcpyAsync(jd, jobs.data(), sizeof(AcqJob) * jobs.size(), hipMemcpyHostToDevice, c->stream));
-    HIPCHK(launch_acquire(c->stream, iq, (const AcqJob *)jd, (int)jobs.size(), c->osc, (AcqResult *)rd));
+    HIPCHK(launch_acquire(c->stream, iq, p->iq_fmt, (const AcqJob *)jd, (int)jobs.size(), c->osc, (AcqResult *)rd));
     std::vector<AcqResult> res(jobs.size());
     HIPCHK(hipMemcpyAsync(res.data(), rd, sizeof(AcqResult) * jobs.size(), hipMemcpyDeviceToHost, c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
@@ -1218,12 +1231,12 @@ static int acquire_streams(dabgpu_pipe *p, const float *iq, int64_t stride, cons
 
 // Background form (DABGPU_CTL_ACQ_ASYNC): the same search launched on the pipeline's
 // acquisition stream without waiting; acq_collect applies the results once they are in.
-static int acquire_streams_async(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
+static int acquire_streams_async(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_t *n_avail,
                                  const std::vector<int> &who, const std::vector<StreamSt> &cur) {
     for (size_t i = 0; i < who.size(); i++) p->h_acq_jobs[i] = acq_job(p, cur[who[i]], who[i], stride, n_avail);
     const size_t n = who.size();
     HIPCHK(hipMemcpyAsync(p->acq_jobs_d, p->h_acq_jobs, sizeof(AcqJob) * n, hipMemcpyHostToDevice, p->as));
-    HIPCHK(launch_acquire(p->as, iq, p->acq_jobs_d, (int)n, p->c->osc, p->acq_res_d));
+    HIPCHK(launch_acquire(p->as, iq, p->iq_fmt, p->acq_jobs_d, (int)n, p->c->osc, p->acq_res_d));
     HIPCHK(hipMemcpyAsync(p->h_acq, p->acq_res_d, sizeof(AcqResult) * n, hipMemcpyDeviceToHost, p->as));
     HIPCHK(hipEventRecord(p->ev_acq, p->as));
     p->acq_who = who;
@@ -1246,7 +1259,7 @@ static int acq_collect(dabgpu_pipe *p, bool wait) {
     return 0;
 }
 
-extern "C" int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *start_h,
+extern "C" int dabgpu_pipe_acquire(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_t *start_h,
                                    const int64_t *n_avail_h) {
     if (!p || !iq || !start_h || !n_avail_h) return fail(DABGPU_E_ARG, "null arg");
     std::vector<int> who;
@@ -1266,7 +1279,7 @@ extern "C" int dabgpu_pipe_acquire(dabgpu_pipe *p, const float *iq, int64_t stri
 // batched kernels, then replays ofdmProcessor::run's sequential logic on the
 // host with the measured values and commits the longest correctly predicted
 // prefix of each stream (ofdm-processor.cpp:344-468).
-static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail,
+static int pipe_front_pass(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_t *n_avail,
                            std::vector<int> &done, std::vector<StreamSt> &cur, bool &progress, bool &lost,
                            const std::function<int()> &after_launch = nullptr) {
     dabgpu_ctx *c = p->c;
@@ -1344,9 +1357,11 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         aux.snr = p->snr_d;
         aux.level = p->threshold;
         aux.disp = p->display ? p->disp_d : nullptr;
+        aux.disp_token = p->disp_token;
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, true));
         const int kChunks = demod_chunks(n, 2);
         aux.ring8 = 1;
+        aux.fmt = p->iq_fmt;
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, (int16_t *)p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         // the host's values and the error word straight into pinned memory (no copies)
@@ -1354,7 +1369,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
                                     p->h_si, p->snr_d, p->h_snr, c->err, c->h_err));
     } else {
         HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, true));
-        HIPCHK(launch_prs_sync(c->stream, iq, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
+        HIPCHK(launch_prs_sync(c->stream, iq, p->iq_fmt, p->frames_d, n, c->T, p->threshold, p->si_d, nullptr, nullptr, general));
         HIPCHK(prof_mark(p, DABGPU_STAGE_PRS, false));
         HIPCHK(hipMemcpyAsync(p->h_si, p->si_d, sizeof(int32_t) * n, hipMemcpyDeviceToHost, c->stream));
     }
@@ -1410,7 +1425,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
     if (n2 && !fast) {
         HIPCHK(hipMemcpyAsync(p->frames_d, fr2.data(), sizeof(dabgpu_frame) * n2, hipMemcpyHostToDevice, c->stream));
         HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, true));
-        HIPCHK(launch_block0(c->stream, iq, p->frames_d, n2, c->T, p->method, p->corr_d, p->snr_d, general));
+        HIPCHK(launch_block0(c->stream, iq, p->iq_fmt, p->frames_d, n2, c->T, p->method, p->corr_d, p->snr_d, general));
         HIPCHK(prof_mark(p, DABGPU_STAGE_BLOCK0, false));
         HIPCHK(hipMemcpyAsync(corr.data(), p->corr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
         HIPCHK(hipMemcpyAsync(snr2.data(), p->snr_d, sizeof(int16_t) * n2, hipMemcpyDeviceToHost, c->stream));
@@ -1465,7 +1480,9 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
         const int kChunks = demod_chunks(n3);
         DemodAux aux{};
         aux.disp = p->display ? p->disp_d : nullptr;
+        aux.disp_token = p->disp_token;
         aux.ring8 = 1;
+        aux.fmt = p->iq_fmt;
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n3, kChunks, c->T, (int16_t *)p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
         HIPCHK(launch_fc_reduce(c->stream, p->fcpart_d, kChunks, n3, p->fc_d));
@@ -1542,7 +1559,7 @@ static int pipe_front_pass(dabgpu_pipe *p, const float *iq, int64_t stride, cons
 
 extern "C" {
 
-int dabgpu_pipe_run(dabgpu_pipe *p, const float *iq, int64_t stride, const int64_t *n_avail, uint8_t *fic_bits,
+int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_t *n_avail, uint8_t *fic_bits,
                     uint8_t *fic_crc, uint8_t *msc_bits, int32_t msc_stride, uint8_t *msc_valid) {
     if (!p || !iq || !n_avail) return fail(DABGPU_E_ARG, "null arg");
     dabgpu_ctx *c = p->c;
@@ -1805,6 +1822,11 @@ int dabgpu_pipe_timing(dabgpu_pipe *p, float *ms, int32_t *launches) {
     return 0;
 }
 
+int dabgpu_pipe_acquire_wait(dabgpu_pipe *p) {
+    if (!p) return fail(DABGPU_E_ARG, "null pipe");
+    return acq_collect(p, true);
+}
+
 int dabgpu_pipe_sync(dabgpu_pipe *p) {
     if (!p) return fail(DABGPU_E_ARG, "null pipe");
     HIPCHK(hipStreamSynchronize(p->c->stream));
@@ -1840,9 +1862,12 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.sf_out = sf_bytes;
     J.sf_stride = sf_stride;
     if (p->dp_compact) {
+        if (p->F > 512) return fail(DABGPU_E_UNSUP, "compact DAB+ output: at most 512 frames per run");
         const size_t need = (size_t)p->S * 4 * p->F * p->NDP * (size_t)sf_stride;
-        if (need > p->sf_sparse_bytes) {             // (stream-ordered: earlier layers are done with it)
-            HIPCHK(hipDeviceSynchronize());
+        if (need > p->sf_sparse_bytes) {
+            // the layers that wrote the old scratch ran on this pipeline's back-end streams:
+            // wait for those (not the whole device: other pipelines, the null search)
+            for (hipStream_t v : p->vs) HIPCHK(hipStreamSynchronize(v));
             if (p->sf_sparse_d) HIPCHK(hipFree(p->sf_sparse_d));
             p->sf_sparse_d = nullptr;
             p->sf_sparse_bytes = 0;
@@ -1852,7 +1877,6 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
         J.sf_out = p->sf_sparse_d;
         J.sf_compact = sf_bytes;
         J.kmax = DABGPU_SF_SLOTS(p->F);
-        if (4 * p->F > 4 * 512) return fail(DABGPU_E_UNSUP, "compact DAB+ output: at most 512 frames per run");
     }
     J.info = info;
     J.tabs = c->dptab;
@@ -1873,6 +1897,9 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
 
 int dabgpu_pipe_state(dabgpu_pipe *p, int s, dabgpu_stream_state *o) {
     if (!p || !o || s < 0 || s >= p->S) return fail(DABGPU_E_ARG, "bad args");
+    // a background null search that has finished is taken now (not at the next run), so
+    // `acquiring` says whether the search still reads iq_d
+    if (int rc = acq_collect(p, false)) return rc;
     const StreamSt &x = p->st[s];
     o->next_pos = x.window;
     o->local_phase = x.lp;
@@ -1938,6 +1965,10 @@ int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op) {
         p->acq_async = true;
         return 0;
     }
+    // a background search in flight carries the stream's old correctors and position: it
+    // completes and is applied first, so the control below is the last word (the reference
+    // runs these methods between its own sequential steps)
+    if (int rc = acq_collect(p, true)) return rc;
     for (int s = (stream < 0 ? 0 : stream); s < (stream < 0 ? p->S : stream + 1); s++) {
         StreamSt &x = p->st[s];
         switch (op) {
@@ -1965,6 +1996,12 @@ int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot) {
 int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on) {
     if (!p) return fail(DABGPU_E_ARG, "bad args");
     p->packed = on != 0;
+    return 0;
+}
+int dabgpu_pipe_set_iq_format(dabgpu_pipe *p, int format) {
+    if (!p || (format != DABGPU_IQ_F32 && format != DABGPU_IQ_S16 && format != DABGPU_IQ_U8))
+        return fail(DABGPU_E_ARG, "bad args");
+    p->iq_fmt = format;
     return 0;
 }
 int dabgpu_pipe_set_dabplus_compact(dabgpu_pipe *p, int on) {
@@ -2005,6 +2042,11 @@ int dabgpu_pipe_set_display(dabgpu_pipe *p, int on) {
         HIPCHK(hipMemset(p->disp_d, 0, sizeof(float2) * (size_t)p->S * p->R * K));
     }
     p->display = on != 0;
+    return 0;
+}
+int dabgpu_pipe_set_display_token(dabgpu_pipe *p, int token) {
+    if (!p || token < 1 || token > NSYM) return fail(DABGPU_E_ARG, "display token %d outside 1..75", token);
+    p->disp_token = token;
     return 0;
 }
 int dabgpu_pipe_iq_display(dabgpu_pipe *p, int stream, int frame, float *carriers_h) {

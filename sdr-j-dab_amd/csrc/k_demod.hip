@@ -344,8 +344,8 @@ __device__ __forceinline__ void soft_pair(float2 r1, float ab1, int &ir, int &ii
 // dump words, each store half-wave's at banks its carriers leave free.
 constexpr int STG = K + 32;
 
-template <bool GEN, bool SYNC, bool R8>
-__global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2 *__restrict__ iq,
+template <bool GEN, bool SYNC, bool R8, int FMT, bool DUMP>
+__global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *__restrict__ iq,
                                                     const dabgpu_frame *__restrict__ frames, int nchunks,
                                                     OfdmTables T, int16_t *__restrict__ soft,
                                                     float *__restrict__ softf, float2 *__restrict__ fcpart,
@@ -368,7 +368,9 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
     const int item = blockIdx.x;
     const int fi = item / nchunks, ch = item % nchunks;
     dabgpu_frame fr = frames[fi];
-    const float2 *s = iq + fr.iq_base;
+    const void *s = iq_stream<FMT>(iq, fr.iq_base);
+    using Fmt = IqFmt<FMT>;
+    constexpr int BPS = Fmt::bps;
     bool skip = false;
     if constexpr (SYNC) {
         // the frame starts where findIndex finds it (block0 = window + startIndex,
@@ -384,7 +386,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         } else {
             float2 a[8];
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
+            for (int m = 0; m < 8; m++) a[m] = iq_at<FMT>(s, fr.window + t + 256 * m);
             mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
             float mx, sm;
             const int32_t si = prs_corr_wg(a, ex, tw, t, T.ref, aux.level, red, mx, sm);
@@ -431,9 +433,9 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
         // the frame's samples and soft-bit rows through buffer descriptors (wave-uniform
         // bases: 32-bit offsets, the 8 samples of a thread a scalar offset apart, no
         // 64-bit address arithmetic per symbol)
-        const float2 *fb = s + fr.block0;
+        const void *fb = (const char *)s + fr.block0 * BPS;
         const __amdgpu_buffer_rsrc_t rin =
-            __builtin_amdgcn_make_buffer_rsrc((void *)fb, (short)0, (TU + NSYM * TS) * 8, 0x00020000);
+            __builtin_amdgcn_make_buffer_rsrc((void *)fb, (short)0, (TU + NSYM * TS) * BPS, 0x00020000);
         // soft-bit rows: int16, or RING8 bytes (v + 127) in the pipeline's ring
         constexpr int esz = R8 ? 1 : 2;
         char *orow = (char *)soft + (int64_t)fr.out_slot * NSYM * SYMBITS * esz;
@@ -445,24 +447,25 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             if constexpr (!R8) return v;
             return __builtin_bit_cast(uint32_t, __builtin_bit_cast(u16x2, v) + (u16x2){RING8_BIAS, RING8_BIAS});
         };
-        auto ld = [&](int32_t off) -> float2 {                      // off: byte offset from block 0
-            return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(rin, off, 0, 0));
-        };
-        float2 a[8], nx[8], P[8], ng6, ng7;
+        // off: byte offset from block 0; the prefetch registers hold the raw samples (8, 4
+        // or 2 bytes), converted when the symbol's turn comes
+        auto ld = [&](int32_t off) -> typename Fmt::raw { return Fmt::load(rin, off); };
+        float2 a[8], P[8];
+        typename Fmt::raw nx[8], ng6, ng7;
         // warm-up symbol l0 - 1 (block 0, the PRS, for the first chunk)
         {
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
-            const int32_t o = ((l0 - 1) * TS + t) * 8;
+            const int32_t o = ((l0 - 1) * TS + t) * BPS;
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = ld(o + 2048 * m);
+            for (int m = 0; m < 8; m++) a[m] = Fmt::cvt(ld(o + 256 * BPS * m));
             if (l0 == 1) mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
             else mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
         }
-        int32_t ov = (l0 * TS + t) * 8;                       // this thread's sample 0 of symbol l
-        ng6 = ld(ov - 4096);
-        ng7 = ld(ov - 2048);
+        int32_t ov = (l0 * TS + t) * BPS;                     // this thread's sample 0 of symbol l
+        ng6 = ld(ov - 512 * BPS);
+        ng7 = ld(ov - 256 * BPS);
 #pragma unroll
-        for (int m = 0; m < 8; m++) nx[m] = ld(ov + 2048 * m);
+        for (int m = 0; m < 8; m++) nx[m] = ld(ov + 256 * BPS * m);
         fft2048_wg(a, ex, tw, t);
         if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
             const int16_t v = snr_wg(a, t, red);
@@ -508,16 +511,16 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
             // this symbol's samples and its guard samples, all loaded one symbol ahead
             // (a guard load issued here would expose a full HBM latency per symbol)
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = nx[m];
-            float2 g6 = ng6, g7 = ng7;
+            for (int m = 0; m < 8; m++) a[m] = Fmt::cvt(nx[m]);
+            const float2 g6 = Fmt::cvt(ng6), g7 = Fmt::cvt(ng7);
             if (l + 1 < l1) {
-                const int32_t o1 = ov + TS * 8;
-                ng6 = ld(o1 - 4096);
-                ng7 = ld(o1 - 2048);
+                const int32_t o1 = ov + TS * BPS;
+                ng6 = ld(o1 - 512 * BPS);
+                ng7 = ld(o1 - 256 * BPS);
 #pragma unroll
-                for (int m = 0; m < 8; m++) nx[m] = ld(o1 + 2048 * m);
+                for (int m = 0; m < 8; m++) nx[m] = ld(o1 + 256 * BPS * m);
             }
-            ov += TS * 8;
+            ov += TS * BPS;
             // FreqCorr over i in [T_u, T_s) on the samples before the NCO: the mixed
             // product x[i] conj(x[i - T_u]) is the raw one times oscillatorTable[-T_u phase]
             // (efc, applied once at the end)
@@ -541,8 +544,13 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
                 }
                 w = cmul_d(w, dr, di);
             }
+            if constexpr (DUMP) {                      // test hook: the FFT's input, mixed
+                float2 *mp = aux.mix + ((int64_t)fr.out_slot * NSYM + (l - 1)) * TU;
+#pragma unroll
+                for (int m = 0; m < 8; m++) mp[t + 256 * m] = a[m];
+            }
             fft2048_wg(a, ex, tw, t);
-            if (l == 2 && aux.disp) {                  // the display token's carriers (ofdm-decoder.cpp:197-205)
+            if (aux.disp && l == aux.disp_token) {     // the display token's carriers (ofdm-decoder.cpp:197-205)
                 float2 *dp = aux.disp + (int64_t)fr.out_slot * K;
                 const int b0 = bin0_of(t);
 #pragma unroll
@@ -646,8 +654,8 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const float2
 
 // findIndex alone, one workgroup per frame (the host needs startIndex before block 0
 // while the coarse AFC is pending)
-template <bool GEN>
-__global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
+template <bool GEN, int FMT>
+__global__ __launch_bounds__(DT) void k_prs_wg(const void *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
                                                OfdmTables T, DemodAux aux) {
     __shared__ float2 ex[EXN];
     __shared__ TwLds twl;
@@ -665,10 +673,10 @@ __global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, co
         }
         return;
     }
-    const float2 *s = iq + fr.iq_base;
+    const void *s = iq_stream<FMT>(iq, fr.iq_base);
     float2 a[8];
 #pragma unroll
-    for (int m = 0; m < 8; m++) a[m] = s[fr.window + t + 256 * m];
+    for (int m = 0; m < 8; m++) a[m] = iq_at<FMT>(s, fr.window + t + 256 * m);
     mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.window + t, fr.window);
     float mx, sm;
     const int32_t si = prs_corr_wg(a, ex, tw, t, T.ref, aux.level, red, mx, sm);
@@ -683,8 +691,8 @@ __global__ __launch_bounds__(DT) void k_prs_wg(const float2 *__restrict__ iq, co
 // (segment A of the NCO), get_snr, and when frames[f].flags & 1 the coarse offset of
 // freqSyncMethod `method` in carriers (100 - 2048 when method 2 finds nothing, 100
 // means "no estimate" for method 1 -- the reference's values).
-template <bool GEN>
-__global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
+template <bool GEN, int FMT>
+__global__ __launch_bounds__(DT) void k_block0_wg(const void *__restrict__ iq, const dabgpu_frame *__restrict__ frames,
                                                   OfdmTables T, int method, int16_t *__restrict__ correction,
                                                   int16_t *__restrict__ snr) {
 #pragma clang fp contract(off)
@@ -708,10 +716,10 @@ __global__ __launch_bounds__(DT) void k_block0_wg(const float2 *__restrict__ iq,
         }
         return;
     }
-    const float2 *s = iq + fr.iq_base;
+    const void *s = iq_stream<FMT>(iq, fr.iq_base);
     float2 a[8];
 #pragma unroll
-    for (int m = 0; m < 8; m++) a[m] = s[fr.block0 + t + 256 * m];
+    for (int m = 0; m < 8; m++) a[m] = iq_at<FMT>(s, fr.block0 + t + 256 * m);
     mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, fr.block0 + t, fr.window);
     fft2048_wg(a, ex, tw, t);
     {
@@ -859,26 +867,45 @@ hipError_t launch_symbol(hipStream_t st, const float *smp, int kind, const OfdmT
     return hipGetLastError();
 }
 
-hipError_t launch_demod(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, int nchunks,
+hipError_t launch_demod(hipStream_t st, const void *iq, const dabgpu_frame *fr, int n, int nchunks,
                         const OfdmTables &T, int16_t *soft, float *softf, float *fcpart, bool general,
                         const DemodAux &aux) {
     if (n <= 0) return hipSuccess;
     const dim3 grid(n * nchunks), block(DT);
-    const float2 *x = (const float2 *)iq;
     float2 *fp = (float2 *)fcpart;
-#define DEMOD_GO(G, S, R) hipLaunchKernelGGL((k_demod_wg<G, S, R>), grid, block, 0, st, x, fr, nchunks, T, soft, softf, fp, aux)
-    if (aux.ring8) {                                   // the pipeline's RING8 ring
-        if (aux.si) { if (general) DEMOD_GO(true, true, true); else DEMOD_GO(false, true, true); }
-        else { if (general) DEMOD_GO(true, false, true); else DEMOD_GO(false, false, true); }
-    } else {
-        if (aux.si) { if (general) DEMOD_GO(true, true, false); else DEMOD_GO(false, true, false); }
-        else { if (general) DEMOD_GO(true, false, false); else DEMOD_GO(false, false, false); }
+#define DEMOD_GO(G, S, R, F, D) \
+    hipLaunchKernelGGL((k_demod_wg<G, S, R, F, D>), grid, block, 0, st, iq, fr, nchunks, T, soft, softf, fp, aux)
+#define DEMOD_GS(R, F)                                              \
+    do {                                                            \
+        if (aux.si) { if (general) DEMOD_GO(true, true, R, F, false); else DEMOD_GO(false, true, R, F, false); } \
+        else { if (general) DEMOD_GO(true, false, R, F, false); else DEMOD_GO(false, false, R, F, false); }     \
+    } while (0)
+    if (aux.mix) {                                     // the NCO test hook: operator form only
+        if (!general || aux.si || aux.ring8 || aux.fmt != DABGPU_IQ_F32) return hipErrorInvalidValue;
+        DEMOD_GO(true, false, false, DABGPU_IQ_F32, true);
+    } else if (aux.ring8) {                            // the pipeline's RING8 ring, any sample format
+        if (aux.fmt == DABGPU_IQ_S16) DEMOD_GS(true, DABGPU_IQ_S16);
+        else if (aux.fmt == DABGPU_IQ_U8) DEMOD_GS(true, DABGPU_IQ_U8);
+        else if (aux.fmt == DABGPU_IQ_F32) DEMOD_GS(true, DABGPU_IQ_F32);
+        else return hipErrorInvalidValue;
+    } else {                                           // the operators: cf32 in, int16 out
+        if (aux.fmt != DABGPU_IQ_F32) return hipErrorInvalidValue;
+        DEMOD_GS(false, DABGPU_IQ_F32);
     }
+#undef DEMOD_GS
 #undef DEMOD_GO
     return hipGetLastError();
 }
 
-hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+#define FMT_DISPATCH(fmt, GO)                                       \
+    do {                                                            \
+        if ((fmt) == DABGPU_IQ_F32) GO(DABGPU_IQ_F32);              \
+        else if ((fmt) == DABGPU_IQ_S16) GO(DABGPU_IQ_S16);         \
+        else if ((fmt) == DABGPU_IQ_U8) GO(DABGPU_IQ_U8);           \
+        else return hipErrorInvalidValue;                           \
+    } while (0)
+
+hipError_t launch_prs_sync(hipStream_t st, const void *iq, int fmt, const dabgpu_frame *fr, int n, const OfdmTables &T,
                            int level, int32_t *si, float *mx, float *sm, bool general) {
     if (n <= 0) return hipSuccess;
     DemodAux aux{};
@@ -886,17 +913,28 @@ hipError_t launch_prs_sync(hipStream_t st, const float *iq, const dabgpu_frame *
     aux.maxv = mx;
     aux.sumv = sm;
     aux.level = level;
-    if (general) hipLaunchKernelGGL(k_prs_wg<true>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, aux);
-    else hipLaunchKernelGGL(k_prs_wg<false>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, aux);
+#define PRS_GO(F)                                                                                   \
+    do {                                                                                            \
+        if (general) hipLaunchKernelGGL((k_prs_wg<true, F>), dim3(n), dim3(DT), 0, st, iq, fr, T, aux);  \
+        else hipLaunchKernelGGL((k_prs_wg<false, F>), dim3(n), dim3(DT), 0, st, iq, fr, T, aux);         \
+    } while (0)
+    FMT_DISPATCH(fmt, PRS_GO);
+#undef PRS_GO
     return hipGetLastError();
 }
 
-hipError_t launch_block0(hipStream_t st, const float *iq, const dabgpu_frame *fr, int n, const OfdmTables &T,
+hipError_t launch_block0(hipStream_t st, const void *iq, int fmt, const dabgpu_frame *fr, int n, const OfdmTables &T,
                          int method, int16_t *corr, int16_t *snr, bool general) {
     if (n <= 0) return hipSuccess;
-    if (general) hipLaunchKernelGGL(k_block0_wg<true>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, method, corr, snr);
-    else hipLaunchKernelGGL(k_block0_wg<false>, dim3(n), dim3(DT), 0, st, (const float2 *)iq, fr, T, method, corr, snr);
+#define B0_GO(F)                                                                                                 \
+    do {                                                                                                         \
+        if (general) hipLaunchKernelGGL((k_block0_wg<true, F>), dim3(n), dim3(DT), 0, st, iq, fr, T, method, corr, snr); \
+        else hipLaunchKernelGGL((k_block0_wg<false, F>), dim3(n), dim3(DT), 0, st, iq, fr, T, method, corr, snr);        \
+    } while (0)
+    FMT_DISPATCH(fmt, B0_GO);
+#undef B0_GO
     return hipGetLastError();
 }
+#undef FMT_DISPATCH
 
 }  // namespace dab

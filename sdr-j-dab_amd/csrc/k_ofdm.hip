@@ -61,7 +61,8 @@ __device__ __forceinline__ float slevel_next(float s, double pj) {
     return (float)(pj + (1 - 0.00001) * (double)s);                // ofdm-processor.cpp:225
 }
 
-__global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, const AcqJob *__restrict__ jobs, int n,
+template <int FMT>
+__global__ __launch_bounds__(64) void k_acquire(const void *__restrict__ iq, const AcqJob *__restrict__ jobs, int n,
                                                 const float2 *__restrict__ osc, AcqResult *__restrict__ res) {
 #pragma clang fp contract(off)
     // a group reads up to 64 samples past its start: the arrays carry 64 zeros behind the block
@@ -80,7 +81,7 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
     // the pipeline's ACS waves fill the SIMDs (a sync loss) is not starved of issue slots
     __builtin_amdgcn_s_setprio(3);
     const AcqJob jb = jobs[blockIdx.x];
-    const float2 *x = iq + jb.iq_base;
+    const void *x = iq_stream<FMT>(iq, jb.iq_base);
     const int32_t ph = jb.phase;
     int64_t a = jb.start, pos = jb.start;            // attempt start, next unread sample
     int32_t lpa = jb.local_phase;                    // localPhase at the attempt start
@@ -104,7 +105,7 @@ __global__ __launch_bounds__(64) void k_acquire(const float2 *__restrict__ iq, c
             for (int r = 0; r < R; r++) {
                 const int i = lane + 64 * r;
                 const int64_t p = pos + (i < nb ? i : 0);
-                xs[r] = x[p];
+                xs[r] = iq_at<FMT>(x, p);
                 os[r] = osc[acq_lp(p, a, lpa, ph)];
             }
 #pragma unroll
@@ -308,10 +309,13 @@ hipError_t launch_fc_reduce(hipStream_t st, const float *part, int nchunks, int 
     hipLaunchKernelGGL(k_fc_reduce, dim3((n + 63) / 64), dim3(64), 0, st, (const float2 *)part, nchunks, n, (float2 *)out);
     return hipGetLastError();
 }
-hipError_t launch_acquire(hipStream_t st, const float *iq, const AcqJob *jobs, int n, const float2 *osc,
+hipError_t launch_acquire(hipStream_t st, const void *iq, int fmt, const AcqJob *jobs, int n, const float2 *osc,
                           AcqResult *res) {
     if (n <= 0) return hipSuccess;
-    hipLaunchKernelGGL(k_acquire, dim3(n), dim3(64), 0, st, (const float2 *)iq, jobs, n, osc, res);
+    if (fmt == DABGPU_IQ_F32) hipLaunchKernelGGL(k_acquire<DABGPU_IQ_F32>, dim3(n), dim3(64), 0, st, iq, jobs, n, osc, res);
+    else if (fmt == DABGPU_IQ_S16) hipLaunchKernelGGL(k_acquire<DABGPU_IQ_S16>, dim3(n), dim3(64), 0, st, iq, jobs, n, osc, res);
+    else if (fmt == DABGPU_IQ_U8) hipLaunchKernelGGL(k_acquire<DABGPU_IQ_U8>, dim3(n), dim3(64), 0, st, iq, jobs, n, osc, res);
+    else return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

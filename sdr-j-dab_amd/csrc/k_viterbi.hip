@@ -546,8 +546,13 @@ __device__ __forceinline__ void acs_tiles_in(const VitJob &J, const Src (&c)[2],
         for (int k = 0; k < IN_K; k++) {
             if (64 * k < I1 - I0) {
                 if constexpr (B8) {
-                    vab[k][0] = __builtin_amdgcn_raw_buffer_load_b8(c[0].rs, oa, 64 * k, 0);
-                    vab[k][1] = __builtin_amdgcn_raw_buffer_load_b8(c[1].rs, ob, 64 * k, 0);
+                    // a refused or empty row (RO_EMPTY: the load is out of bounds and returns
+                    // 0, which as a RING8 byte is soft value -127) reads the erasure byte 127,
+                    // as the int16 form reads the erasure 0
+                    const uint32_t a8 = __builtin_amdgcn_raw_buffer_load_b8(c[0].rs, oa, 64 * k, 0);
+                    const uint32_t b8 = __builtin_amdgcn_raw_buffer_load_b8(c[1].rs, ob, 64 * k, 0);
+                    vab[k][0] = ro.x == RO_EMPTY ? (uint16_t)RING8_BIAS : (uint16_t)a8;
+                    vab[k][1] = ro.y == RO_EMPTY ? (uint16_t)RING8_BIAS : (uint16_t)b8;
                 } else {
                     vab[k][0] = __builtin_amdgcn_raw_buffer_load_b16(c[0].rs, oa, 128 * k, 0);
                     vab[k][1] = __builtin_amdgcn_raw_buffer_load_b16(c[1].rs, ob, 128 * k, 0);

@@ -99,6 +99,8 @@ def lib() -> C.CDLL:
             "dabgpu_ofdm_symbol": ([vp, vp, i32, vp, vp], i32),
             "dabgpu_get_snr": ([vp, vp, vp], i32),
             "dabgpu_nco_eval": ([vp, i32, i32, vp], i32),
+            "dabgpu_ofdm_demod_mix": ([vp, vp, vp, i32, i32, vp, vp], i32),
+            "dabgpu_pipe_set_iq_format": ([vp, i32], i32),
             "dabgpu_iq_convert": ([vp, i32, vp, i64, vp], i32),
             "dabgpu_event_record": ([vp, i32], i32),
             "dabgpu_kernel_errors": ([vp], i32),
@@ -154,7 +156,7 @@ def _p(a: np.ndarray) -> C.c_void_p:
     return C.c_void_p(a.ctypes.data)
 
 
-IQ_U8, IQ_S16 = 1, 2   # dabgpu_iq_convert formats
+IQ_F32, IQ_U8, IQ_S16 = 0, 1, 2   # sample formats (dabgpu_iq_convert, dabgpu_pipe_set_iq_format)
 TABLE_PRS, TABLE_MAPPER, TABLE_REFARG, TABLE_OSC, TABLE_NCO = 1, 2, 3, 4, 5
 
 
@@ -465,6 +467,25 @@ class Context:
                     b.free()
 
 
+    def demod_mix(self, iq: DevBuf, frames: Sequence[Frame], chunks: int = 1):
+        """dabgpu_ofdm_demod_mix: the fused demod's NCO-mixed FFT input of every data
+        symbol, complex64 [n, 75, 2048] (samples [T_g, T_s) of symbol l after getSamples'
+        NCO), and the int16 soft bits [n, 75, 3072]; `chunks` workgroups per frame"""
+        n = len(frames)
+        fa = (Frame * n)(*frames)
+        dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
+        dm = self.buf(8 * n * NSYM * 2048)
+        ds = self.buf(2 * n * NSYM * SYMBITS)
+        try:
+            _chk(lib().dabgpu_ofdm_demod_mix(self.h, iq.ptr, dfr.ptr, n, chunks, dm.ptr, ds.ptr), "ofdm_demod_mix")
+            mix = dm.download(np.float32, (n, NSYM, 2048, 2))
+            soft = ds.download(np.int16, (n, NSYM, SYMBITS))
+            self.check()
+            return mix, soft
+        finally:
+            for b in (dfr, dm, ds):
+                b.free()
+
     def nco_eval(self, first: int = 0, n: int = 2048000) -> np.ndarray:
         """oscillatorTable[first:first+n] as the front-end kernels compute it
         (dabgpu_nco_eval): float32 [n, 2]"""
@@ -642,6 +663,13 @@ class Pipeline:
         msc [S, 4F, n_subch, msc_stride_packed] bytes"""
         _chk(lib().dabgpu_pipe_set_packed(self.h, int(on)), "dabgpu_pipe_set_packed")
         self.packed = bool(on)
+
+    def set_iq_format(self, fmt: int) -> None:
+        """sample format of the streams acquire() / run() read: IQ_F32 (default), IQ_S16
+        (.sdr PCM16) or IQ_U8 (.raw), converted exactly in the kernels' loads
+        (dabgpu_pipe_set_iq_format); strides and n_avail stay in samples"""
+        _chk(lib().dabgpu_pipe_set_iq_format(self.h, int(fmt)), "dabgpu_pipe_set_iq_format")
+        self.iq_format = int(fmt)
 
     def fetch(self, dst: "HostBuf", src: DevBuf, nbytes: int, dst_off: int = 0) -> None:
         """asynchronous copy of an output of the last run to pinned host memory, behind

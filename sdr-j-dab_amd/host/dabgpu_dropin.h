@@ -336,9 +336,13 @@ public:
     // get_snr (ofdm-decoder.cpp:212-230) of a T_u-point spectrum (natural bin order)
     int16_t get_snr(DSPCOMPLEX *v);
     int16_t snr() const { return snr_; }
+    // the symbol whose carriers feed iqBuffer (ofdm-decoder.cpp:61,197; the reference
+    // declares set_displayToken, ofdm-decoder.h:50, without defining it: here it works)
+    void set_displayToken(int16_t t) { displayToken = t; }
     // processToken's `static int cnt` (ofdm-decoder.cpp:171): one count per process
     static std::atomic<int> iq_count;
-    static constexpr int16_t displayToken = 2;                 // ofdm-decoder.cpp:63
+    static constexpr int16_t defaultDisplayToken = 2;          // ofdm-decoder.cpp:61
+    int16_t displayToken = defaultDisplayToken;
 private:
     uint8_t method_;
     RingBuffer<DSPCOMPLEX> *iqBuffer_ = nullptr;
@@ -389,6 +393,10 @@ public:
     void startDumping(SNDFILE *f);
     void startDumping(FILE *f);
     void stopDumping();
+    // the display symbol of the decoder this processor drives (ofdmDecoder::set_displayToken,
+    // ofdm-decoder.h:50; the reference's ofdmProcessor owns its ofdmDecoder): 1..75, from
+    // the next frame on
+    void set_displayToken(int16_t t) { displayToken_ = t; }
     int64_t frames() const { return frames_.load(); }
     static constexpr int32_t spectrumSize = 32768;          // bufferSize (ofdm-processor.cpp:97)
 private:
@@ -414,6 +422,7 @@ private:
     std::atomic<FILE *> dumpFile_{nullptr};
     std::atomic<SNDFILE *> dumpSnd_{nullptr};
     int16_t dumpScaler_ = 512;
+    std::atomic<int16_t> displayToken_{ofdmDecoder::defaultDisplayToken};
     // observables state
     int64_t last_block0_ = -1;
     int32_t avgTokenLength_ = 196608, tokenCount_ = 0;

@@ -362,6 +362,8 @@ void ofdmProcessor::run() {                                        // ofdm-proce
         last_run = end;
         // decode every frame the samples so far allow, one per pipeline run
         for (;;) {
+            const int16_t token = displayToken_.load();
+            if (iqBuffer_) chk(dabgpu_pipe_set_display_token(pipe, token), "dabgpu_pipe_set_display_token");
             const float *iq = (const float *)bufs[cur].get() - 2 * base;
             win_ = (const float *)bufs[cur].get();
             win_base_ = base;
@@ -407,7 +409,7 @@ void ofdmProcessor::run() {                                        // ofdm-proce
                     msc_->process_mscBlock(ib, blk);
                 }
                 // processToken's display token (ofdm-decoder.cpp:192-206), exported by the demod
-                if (blk == ofdmDecoder::displayToken && ++ofdmDecoder::iq_count > 7) {
+                if (blk == token && ++ofdmDecoder::iq_count > 7) {
                     ofdmDecoder::iq_count = 0;
                     if (iqBuffer_) {
                         chk(dabgpu_pipe_iq_display(pipe, 0, 0, (float *)carriers.data()), "dabgpu_pipe_iq_display");

@@ -33,6 +33,9 @@ def oracle():
         _o.orc_process_block0.restype = C.c_int16
         _o.orc_rs_dec.restype = C.c_int16
         _o.orc_ofdm_run.argtypes = [C.c_void_p, C.c_int64, C.c_int16, C.c_int, C.c_int, C.c_void_p, C.c_void_p]
+        _o.orc_ofdm_run_fft.argtypes = [C.c_void_p, C.c_int64, C.c_int16, C.c_int, C.c_int, C.c_void_p, C.c_void_p,
+                                        C.c_int]
+        _o.orc_process_block0_fft.restype = C.c_int16
         _o.orc_null_scan.argtypes = [C.c_void_p, C.c_int64, C.c_int, C.c_void_p, C.c_void_p, C.c_void_p]
         _o.orc_get_snr.restype = C.c_int16
         _o.orc_init()           # tables built once: the functions are then safe from threads
@@ -76,10 +79,16 @@ def msc_deconvolve(uep, bitrate, plevel, frag):
     return out ^ prbs(nb)
 
 
-def ofdm_run(iq, max_frames, threshold=3, method=1):
+def ofdm_run(iq, max_frames, threshold=3, method=1, fft_kind=0):
+    """ofdmProcessor::run over a cf32 stream; fft_kind 1 runs it with the fp32 radix-4 FFT
+    (orc_fft2048_f32, FFTW3f's precision class: the CPU baseline) instead of the double one"""
     info = (FrameInfo * max_frames)()
     soft = np.zeros((max_frames, 75, 3072), np.int16)
-    n = oracle().orc_ofdm_run(P(iq), C.c_int64(len(iq) // 2), threshold, method, max_frames, info, P(soft))
+    if fft_kind:
+        n = oracle().orc_ofdm_run_fft(P(iq), C.c_int64(len(iq) // 2), threshold, method, max_frames, info, P(soft),
+                                      fft_kind)
+    else:
+        n = oracle().orc_ofdm_run(P(iq), C.c_int64(len(iq) // 2), threshold, method, max_frames, info, P(soft))
     return n, list(info)[:n], soft[:n]
 
 
@@ -112,17 +121,25 @@ def null_scan(iq, n, scan=True):
     return found, a.value, ns.value, pos.value
 
 
-def process_token(sym_ts, phase_ref):
-    """returns ibits, softf; updates phase_ref (cf32 float array [4096]) in place"""
+def process_token(sym_ts, phase_ref, fft_kind=0):
+    """returns ibits, softf; updates phase_ref (cf32 float array [4096]) in place.  fft_kind 1:
+    the fp32 radix-4 FFT (the soft values' fp32 floor) instead of the double one"""
     ib = np.zeros(3072, np.int16)
     sf = np.zeros(3072, np.float32)
-    oracle().orc_process_token(P(np.ascontiguousarray(sym_ts, np.float32)), P(phase_ref), P(ib), P(sf))
+    if fft_kind:
+        oracle().orc_process_token_fft(P(np.ascontiguousarray(sym_ts, np.float32)), P(phase_ref), P(ib), P(sf),
+                                       fft_kind)
+    else:
+        oracle().orc_process_token(P(np.ascontiguousarray(sym_ts, np.float32)), P(phase_ref), P(ib), P(sf))
     return ib, sf
 
 
-def process_block0(blk, flag=1, method=1):
+def process_block0(blk, flag=1, method=1, fft_kind=0):
     pr = np.zeros(4096, np.float32)
-    c = oracle().orc_process_block0(P(np.ascontiguousarray(blk, np.float32)), P(pr), flag, method)
+    if fft_kind:
+        c = oracle().orc_process_block0_fft(P(np.ascontiguousarray(blk, np.float32)), P(pr), flag, method, fft_kind)
+    else:
+        c = oracle().orc_process_block0(P(np.ascontiguousarray(blk, np.float32)), P(pr), flag, method)
     return c, pr
 
 
@@ -170,10 +187,11 @@ def get_snr(spectrum):
     return int(oracle().orc_get_snr(P(np.ascontiguousarray(spectrum, np.float32))))
 
 
-def fft(x):
-    """the oracle's 2048-point FFT (double precision, rounded to float) of cf32 [4096]"""
+def fft(x, inverse=False, fft_kind=0):
+    """the oracle's 2048-point FFT of cf32 [4096]: double precision rounded to float
+    (fft_kind 0), the fp32 radix-4 Stockham transform (1), fp32 radix-2 DIT (2) / DIF (3)"""
     out = np.zeros(4096, np.float32)
-    oracle().orc_fft2048(P(np.ascontiguousarray(x, np.float32)), P(out), 0)
+    oracle().orc_fft2048_kind(P(np.ascontiguousarray(x, np.float32)), P(out), int(inverse), int(fft_kind))
     return out
 
 

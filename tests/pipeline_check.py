@@ -9,26 +9,60 @@ import numpy as np
 
 import oracle_py as orc
 
+IQ_F32, IQ_U8, IQ_S16 = 0, 1, 2                  # dabgpu.h DABGPU_IQ_*
+
+
+def quantize(iq, fmt):
+    """the cf32 samples a recorded format carries: .sdr PCM16 (x -> round(32768 x),
+    read back as / 32768, wavfiles.cpp:172) or .raw u8 (x -> round(128 x + 128), read back
+    as float(v - 128) / 128.0, rawfiles.cpp:115-117), clipped to the format's range; F32
+    unchanged.  The oracle decodes these floats, the GPU the raw samples (to_raw)."""
+    x = np.asarray(iq, np.float32)
+    if fmt == IQ_S16:
+        return (np.clip(np.rint(x * 32768.0), -32768, 32767) / 32768.0).astype(np.float32)
+    if fmt == IQ_U8:
+        return ((np.clip(np.rint(x * 128.0 + 128.0), 0, 255) - 128.0) / 128.0).astype(np.float32)
+    return x
+
+
+def to_raw(iq, fmt):
+    """the raw samples of quantize(iq, fmt) (exact: asserts that iq is representable)"""
+    x = np.asarray(iq, np.float32)
+    if fmt == IQ_S16:
+        r = np.rint(x * 32768.0).astype(np.int16)
+        assert np.array_equal(r.astype(np.float32) / 32768.0, x)
+        return r
+    if fmt == IQ_U8:
+        r = np.rint(x * 128.0 + 128.0).astype(np.uint8)
+        assert np.array_equal((r.astype(np.float32) - 128.0) / 128.0, x)
+        return r
+    return x
+
 
 def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=(), dabplus=False, packed=False,
-               acq_async=False, packed_pad=0):
+               acq_async=False, packed_pad=0, iq_format=IQ_F32):
     """Decode `runs` x F frames of every stream.  iqs: list of float32 IQ arrays
     (interleaved); n_avail: optional list (per run) of per-stream available sample
-    counts.  Returns per stream: dict(info [frames], fic, crc, msc {cif: [nsub][nb]},
+    counts.  iq_format: the streams go to the GPU as that recorded format (iqs must be
+    representable: quantize()), read by the kernels through dabgpu_pipe_set_iq_format.
+    Returns per stream: dict(info [frames], fic, crc, msc {cif: [nsub][nb]},
     soft {frame: [75][3072]} for soft_streams, sf {cif: [(info, bytes)...]})."""
     import dabamd
     S = len(iqs)
     lens = [len(x) // 2 for x in iqs]
     stride = max(lens)
-    buf = np.zeros((S, 2 * stride), np.float32)
+    dt = {IQ_F32: np.float32, IQ_S16: np.int16, IQ_U8: np.uint8}[iq_format]
+    buf = np.zeros((S, 2 * stride), dt)
     for s, x in enumerate(iqs):
-        buf[s, :len(x)] = x
+        buf[s, :len(x)] = to_raw(x, iq_format)
     diq = ctx.put(buf)
     del buf
     subs = [dabamd.Subch(sc[0], sc[1], sc[2], sc[3], 0 if sc[4] else 1,
                          dabamd.SUBCH_DABPLUS if (len(sc) > 5 and sc[5]) else 0) for sc in subch]
     dpi = [k for k, sc in enumerate(subch) if len(sc) > 5 and sc[5]]
     pipe = dabamd.Pipeline(ctx, S, F, subs, freq_sync_method=method)
+    if iq_format != IQ_F32:
+        pipe.set_iq_format(iq_format)
     if packed:                  # MSC bits 8 per byte (dabgpu_pipe_set_packed), unpacked here
         pipe.set_packed(True)
         pipe.msc_stride_packed += packed_pad    # a row stride that is not a multiple of 4 bytes

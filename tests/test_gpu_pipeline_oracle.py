@@ -10,7 +10,14 @@ The oracle decodes the SAME IQ sequentially (oracle_py.decode_stream: ofdmProces
 compared with what the reference's own decoding of its own soft bits gives.  Bar:
 frame placement and correctors identical; decoded FIC/MSC bits and CRC flags
 identical (0 mismatches); int16 soft bits identical except +-1 where the FFT rounding
-(FFTW3f in the reference, absent here: unpinned) moves q*127 across an integer."""
+(FFTW3f in the reference, absent here: unpinned) moves q*127 across an integer.
+
+Every pipeline test runs on cf32 streams and on the same streams stored as .sdr PCM16
+samples (dabgpu_pipe_set_iq_format(DABGPU_IQ_S16): the kernels convert x / 32768 in their
+loads); the quantised floats are what the oracle decodes, so the bar is unchanged.  A
+subset also runs on .raw u8 samples (rawfiles.cpp:115-117).  The synthetic transmitter's
+amplitude is 0.25 for the recorded formats (peaks inside +-1, as a recording's gain
+would set them)."""
 import numpy as np
 import pytest
 
@@ -30,13 +37,22 @@ def ctx():
     c.close()
 
 
-def _gen(subch, frames, seeds, snr, cfo=0.0):
+F32, S16, U8 = pc.IQ_F32, pc.IQ_S16, pc.IQ_U8
+FMTS = pytest.mark.parametrize("fmt", [F32, S16], ids=["f32", "s16"])
+
+
+def _amp(fmt):
+    return 1.0 if fmt == F32 else 0.25
+
+
+def _gen(subch, frames, seeds, snr, cfo=0.0, fmt=F32):
+    """synthetic streams as the format carries them (pc.quantize)"""
     from dabamd.synth import Ensemble
-    e = Ensemble(frames, subch=subch, snr_db=snr, cfo_hz=cfo)
+    e = Ensemble(frames, subch=subch, snr_db=snr, cfo_hz=cfo, amplitude=_amp(fmt))
     if len(seeds) > 4:
         iq = e.generate_many(len(seeds), seed0=seeds[0], threads=16)
-        return [iq[i] for i in range(len(seeds))]
-    return [e.generate(s, truth=False)["iq"] for s in seeds]
+        return [pc.quantize(iq[i], fmt) for i in range(len(seeds))]
+    return [pc.quantize(e.generate(s, truth=False)["iq"], fmt) for s in seeds]
 
 
 def _check(stats, what, soft=True):
@@ -54,10 +70,11 @@ MIXED = [(0, 96, 128, 3, 1), (96, 48, 64, 0o103, 0), (144, 24, 32, 0o104, 0), (1
          (768, 96, 128, 3, 1)]
 
 
+@FMTS
 @pytest.mark.parametrize("snr,cfo,runs", [(11.0, 0.0, 3), (8.0, 0.0, 3), (12.0, 300.0, 8), (12.0, 800.0, 8),
                                           (11.5, -1700.0, 8), (25.0, 2300.0, 3), (20.0, -9700.0, 4),
                                           (20.0, 6400.0, 4)])
-def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs):
+def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs, fmt):
     """two ensembles, 5 subchannels (UEP-3/-2, EEP-3A/-4A, one above CU 511), runs of 4
     frames: every committed frame's placement/correctors, soft bits, FIC bits + CRCs and
     MSC bits against the oracle run on the same IQ.  8 dB is at the FIC's decoding
@@ -66,12 +83,12 @@ def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs):
     +6.4 kHz are several carriers off: the coarse corrector (processBlock_0's offset,
     ofdm-processor.cpp:395-406) has to move first."""
     F = 4
-    iqs = _gen(MIXED, F * runs + 1, [31, 32], snr, cfo)
+    iqs = _gen(MIXED, F * runs + 1, [31, 32], snr, cfo, fmt)
     refs = orc.decode_streams(iqs, F * runs, MIXED)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, MIXED, soft_streams=(0, 1))
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, MIXED, soft_streams=(0, 1), iq_format=fmt)
     stats = [pc.compare(gpu[s], refs[s], MIXED) for s in range(2)]
-    print(f"snr {snr} cfo {cfo}:", stats)
-    _check(stats, (snr, cfo))
+    print(f"snr {snr} cfo {cfo} fmt {fmt}:", stats)
+    _check(stats, (snr, cfo, fmt))
     if abs(cfo) > 2000.0:
         return                        # the reference's AFC may wander here; parity is what counts
     for s in range(2):
@@ -82,22 +99,58 @@ def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs):
     ctx.check()
 
 
+@FMTS
+def test_pipeline_corrector_sequence_under_drifting_cfo(ctx, fmt):
+    """the AFC loop over a long run (40 frames) under a carrier offset that DRIFTS from +900
+    to +1,150 Hz (a linear chirp applied to the transmitted signal, 6 Hz per frame: the
+    loop's 10 % gain lags it by ~60 Hz, within DQPSK's reach): the fine corrector
+    (ofdm-processor.cpp:445-446, int16 truncation of 0.1 arg(FreqCorr) / pi * 500) steps
+    every frame and wraps into the coarse one past +-500 Hz (:458-466), and FreqCorr is
+    accumulated by the GPU in its own order (raw samples, rotated once) -- the
+    per-frame (coarse, fine) sequence, frame placement and decoded bits must equal the
+    oracle's ofdmProcessor::run frame for frame"""
+    from dabamd.synth import Ensemble
+    sub = MIXED[:2]
+    F, runs = 4, 10
+    e = Ensemble(F * runs + 2, subch=sub, snr_db=15.0, amplitude=_amp(fmt))
+    g = e.generate(81, truth=False)
+    x = g["iq"].reshape(-1, 2).astype(np.float64)
+    n = np.arange(len(x), dtype=np.float64)
+    f0, f1 = 900.0, 1150.0
+    rate = (f1 - f0) / (len(x) / 2048000.0)                 # Hz per second
+    ph = 2 * np.pi * (f0 * n + 0.5 * rate * n * n / 2048000.0) / 2048000.0
+    z = (x[:, 0] + 1j * x[:, 1]) * np.exp(1j * ph)
+    iq = pc.quantize(np.stack([z.real, z.imag], axis=1).astype(np.float32).reshape(-1), fmt)
+    ref = orc.decode_stream(iq, F * runs, sub)
+    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt)
+    st = pc.compare(gpu[0], ref, sub)
+    seq = [(fi.coarse, fi.fine) for fi in gpu[0]["info"]]
+    print("drifting CFO:", st, "correctors", seq[::4])
+    _check([st], ("drift", fmt))
+    assert st["frames"] == ref["n"] >= F * runs - 2
+    assert seq == [(fi.coarse, fi.fine) for fi in ref["info"][:len(seq)]]
+    fines = [f for _, f in seq]
+    assert len(set(fines)) > 10 and len({c for c, _ in seq}) >= 2     # the loop moved, coarse included
+
+
+@FMTS
 @pytest.mark.parametrize("method", [0, 2])
-def test_pipeline_freq_sync_methods(ctx, method):
+def test_pipeline_freq_sync_methods(ctx, method, fmt):
     """freqSyncMethod 0 (getMiddle) and 2 (pattern match) in processBlock_0
     (ofdm-decoder.cpp:103-104,128-161,233-258) through the pipeline under CFO"""
     F, runs = 3, 2
     sub = MIXED[:2]
-    iqs = _gen(sub, F * runs + 1, [41], 20.0, 1200.0)
+    iqs = _gen(sub, F * runs + 1, [41], 20.0, 1200.0, fmt)
     ref = orc.decode_stream(iqs[0], F * runs, sub, method=method)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, method=method)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, method=method, iq_format=fmt)
     st = pc.compare(gpu[0], ref, sub, check_soft=False)
     print("method", method, st)
     _check([st], method, soft=False)
     assert st["frames"] == ref["n"]
 
 
-def test_pipeline_dropout_reacquires_like_reference(ctx):
+@FMTS
+def test_pipeline_dropout_reacquires_like_reference(ctx, fmt):
     """1.5 frames of the signal replaced by an interferer (a carrier at +100 kHz: its
     PRS correlation is flat, so findIndex fails -- Max < 3 * mean): the stream goes back
     to the null search from where it is (goto notSynced), which finds the next null once
@@ -106,7 +159,7 @@ def test_pipeline_dropout_reacquires_like_reference(ctx):
     from dabamd.synth import Ensemble
     sub = MIXED[:2]
     F, runs = 4, 3
-    e = Ensemble(F * runs + 4, subch=sub, snr_db=20.0)
+    e = Ensemble(F * runs + 4, subch=sub, snr_db=20.0, amplitude=_amp(fmt))
     g = e.generate(51, truth=False)
     iq = g["iq"].reshape(-1, 2).copy()
     a = g["frame0"] + 3 * 196608 + 40000
@@ -118,9 +171,9 @@ def test_pipeline_dropout_reacquires_like_reference(ctx):
     rng = np.random.default_rng(5)
     iq[a:b, 0] = level * np.cos(ph) + rng.normal(0, level / 10, b - a)
     iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
-    iq = np.ascontiguousarray(iq.reshape(-1))
+    iq = pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt)
     ref = orc.decode_stream(iq, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,))
+    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt)
     st = pc.compare(gpu[0], ref, sub)
     print("dropout:", st, [(x.resyncs, x.acquisitions, x.frames_run) for x in gpu[0]["states"]])
     _check([st], "dropout")
@@ -131,7 +184,8 @@ def test_pipeline_dropout_reacquires_like_reference(ctx):
     assert any(w2 - w1 != 196608 for w1, w2 in zip(wins, wins[1:]))    # the dropout broke the frame grid
 
 
-def test_pipeline_background_reacquisition_like_reference(ctx):
+@FMTS
+def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
     """DABGPU_CTL_ACQ_ASYNC: stream 0 loses sync in a dropout (as above); its null search
     runs in the background while stream 1 keeps decoding n_frames per run, and the runs
     after the search continue stream 0 from the null it found -- both streams' frames
@@ -140,7 +194,7 @@ def test_pipeline_background_reacquisition_like_reference(ctx):
     from dabamd.synth import Ensemble
     sub = MIXED[:2]
     F, runs = 4, 7
-    e = Ensemble(F * runs + 4, subch=sub, snr_db=20.0)
+    e = Ensemble(F * runs + 4, subch=sub, snr_db=20.0, amplitude=_amp(fmt))
     g0, g1 = e.generate(51, truth=False), e.generate(52, truth=False)
     iq = g0["iq"].reshape(-1, 2).copy()
     a = g0["frame0"] + 3 * 196608 + 40000
@@ -150,9 +204,9 @@ def test_pipeline_background_reacquisition_like_reference(ctx):
     rng = np.random.default_rng(5)
     iq[a:b, 0] = level * np.cos(ph) + rng.normal(0, level / 10, b - a)
     iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
-    iqs = [np.ascontiguousarray(iq.reshape(-1)), g1["iq"]]
+    iqs = [pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt), pc.quantize(g1["iq"], fmt)]
     refs = orc.decode_streams(iqs, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), acq_async=True)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), acq_async=True, iq_format=fmt)
     runs0 = [(x.frames_run, x.acquiring, x.resyncs) for x in gpu[0]["states"]]
     print("background re-acquisition:", runs0)
     assert all(x.frames_run == F for x in gpu[1]["states"])          # stream 1 never waits
@@ -166,18 +220,19 @@ def test_pipeline_background_reacquisition_like_reference(ctx):
     assert st0["frames"] > 4                   # frames after the dropout were decoded too
 
 
-def test_pipeline_streams_out_of_lockstep(ctx):
+@FMTS
+def test_pipeline_streams_out_of_lockstep(ctx, fmt):
     """stream 1 gets fewer samples in run 1 (it commits fewer frames, DABGPU_E_STATE),
     then all of them: its CIF count, 16-CIF de-interleaver and warm-up follow its own
     frames, and run 2's MSC bits of BOTH streams equal the reference path's"""
     sub = MIXED[:3]
     F = 3
-    iqs = _gen(sub, 3 * F + 1, [61, 62], 30.0)
+    iqs = _gen(sub, 3 * F + 1, [61, 62], 30.0, fmt=fmt)
     n = len(iqs[0]) // 2
     refs = orc.decode_streams(iqs, 3 * F, sub)
     fi = refs[1]["info"][1]                    # stream 1 gets samples up to the end of its 2nd frame
     short = fi.window_start + fi.start_index + 2048 + 75 * 2552 + 10
-    gpu = pc.gpu_decode(ctx, iqs, F, 3, sub, n_avail=[[n, short], [n, n], [n, n]])
+    gpu = pc.gpu_decode(ctx, iqs, F, 3, sub, n_avail=[[n, short], [n, n], [n, n]], iq_format=fmt)
     assert gpu[1]["states"][0].frames_run < F and gpu[0]["states"][0].frames_run == F
     for s in range(2):
         st = pc.compare(gpu[s], refs[s], sub, check_soft=False)
@@ -186,32 +241,34 @@ def test_pipeline_streams_out_of_lockstep(ctx):
         assert st["msc_cw"] > 0
 
 
-def test_c3_full_size_bits_match_reference_path(ctx):
+@pytest.mark.parametrize("fmt", [F32, S16, U8], ids=["f32", "s16", "u8"])
+def test_c3_full_size_bits_match_reference_path(ctx, fmt):
     """config C3 at its size: 64 ensembles x 9 UEP-3 128 kbit/s subchannels (all 864
     CUs), 3 runs of 3 frames (36 CIFs: 20 past the 16-CIF warm-up), 12 dB SNR.  Every
     ensemble's FIC and MSC bits against the reference path; soft bits of 4 ensembles."""
     sub = [(96 * i, 96, 128, 3, 1) for i in range(9)]
     F, runs, E = 3, 3, 64
-    iqs = _gen(sub, F * runs + 1, list(range(7000, 7000 + E)), 12.0)
+    iqs = _gen(sub, F * runs + 1, list(range(7000, 7000 + E)), 12.0, fmt=fmt)
     refs = orc.decode_streams(iqs, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 21, 42, 63))
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 21, 42, 63), iq_format=fmt)
     stats = [pc.compare(gpu[s], refs[s], sub) for s in range(E)]
     tot = {k: sum(r[k] for r in stats) for k in ("frames", "fic_cw", "msc_cw", "fic_bad", "msc_bad", "soft", "soft_bad")}
-    print("C3:", tot)
+    print("C3 fmt", fmt, tot)
     _check(stats, "C3")
     assert tot["msc_cw"] == E * 9 * (4 * F * runs - 16)
 
 
-def test_c5_full_size_superframes_match_reference_path(ctx):
+@FMTS
+def test_c5_full_size_superframes_match_reference_path(ctx, fmt):
     """config C5 at its size: 16 ensembles x 16 DAB+ 64 kbit/s EEP-3A subchannels = 256,
     3 runs of 3 frames at 11 dB: MSC bits and every superframe record (fire code, RS
     corrections, AU table, AU CRCs, bytes) against the oracle's mp4Processor fed with
     the ORACLE's own MSC bits"""
     sub = [(48 * i, 48, 64, 0o103, 0, 1) for i in range(16)]
     F, runs, E = 3, 3, 16
-    iqs = _gen(sub, F * runs + 1, list(range(8000, 8000 + E)), 11.0)
+    iqs = _gen(sub, F * runs + 1, list(range(8000, 8000 + E)), 11.0, fmt=fmt)
     refs = orc.decode_streams(iqs, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True, iq_format=fmt)
     n = bad = ok3 = 0
     for s in range(E):
         st = pc.compare(gpu[s], refs[s], sub, check_soft=False)
@@ -222,8 +279,8 @@ def test_c5_full_size_superframes_match_reference_path(ctx):
     assert bad == 0 and ok3 > 0
 
 
-@pytest.mark.parametrize("pad", [0, 1])
-def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad):
+@pytest.mark.parametrize("pad,fmt", [(0, F32), (1, F32), (0, S16), (0, U8)])
+def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad, fmt):
     """dabgpu_pipe_set_packed: the traceback writes the MSC bits 8 per byte (msb first,
     mp4processor.cpp:115-121's packing) and the DAB+ layer reads those bytes -- FIC, MSC
     and every superframe record equal the reference path, with UEP/EEP and DAB+
@@ -234,9 +291,9 @@ def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad):
     sub = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 1), (144, 24, 32, 0o104, 0, 0), (168, 36, 48, 0o103, 0, 1),
            (768, 96, 128, 3, 1, 0)]
     F, runs = 4, 5
-    iqs = _gen(sub, F * runs + 1, [61, 62], 11.0)
+    iqs = _gen(sub, F * runs + 1, [61, 62], 11.0, fmt=fmt)
     refs = orc.decode_streams(iqs, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True, packed=packed, packed_pad=pad)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, dabplus=True, packed=packed, packed_pad=pad, iq_format=fmt)
     ok3 = 0
     for s in range(2):
         st = pc.compare(gpu[s], refs[s], sub, check_soft=False)
@@ -246,6 +303,41 @@ def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad):
         assert bad == 0, (s, n, bad)
         ok3 += c
     assert ok3 > 0
+
+
+@pytest.mark.parametrize("fmt", [S16, U8], ids=["s16", "u8"])
+def test_recorded_format_decodes_like_converted_cf32(ctx, fmt):
+    """the pipeline reading .sdr / .raw samples straight from HBM (the conversion inside
+    the kernels' loads) against the same pipeline reading those samples converted to cf32
+    by dabgpu_iq_convert: frame placement, correctors, every int16 soft bit, FIC and MSC
+    bits identical -- the format is a transport, not an approximation -- under a carrier
+    offset (the NCO path) and noise"""
+    import dabamd
+    sub = MIXED[:3]
+    F, runs = 4, 4
+    iqs = _gen(sub, F * runs + 1, [71, 72], 12.0, 800.0, fmt)
+    raw = [pc.to_raw(x, fmt) for x in iqs]
+    conv = []
+    for r in raw:                                      # dabgpu_iq_convert on the device
+        src = ctx.put(r)
+        dst = ctx.buf(4 * len(r))
+        ctx.iq_convert(fmt, src, len(r) // 2, dst)
+        ctx.sync()
+        conv.append(dst.download(np.float32, (len(r),)))
+        src.free(); dst.free()
+        assert np.array_equal(conv[-1], iqs[len(conv) - 1])
+    a = pc.gpu_decode(ctx, conv, F, runs, sub, soft_streams=(0, 1))
+    b = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), iq_format=fmt)
+    for s in range(2):
+        assert len(a[s]["info"]) == len(b[s]["info"]) >= F * runs - 4
+        for x, y in zip(a[s]["info"], b[s]["info"]):
+            assert (x.window, x.start_index, x.coarse, x.fine, x.correction, x.snr) == \
+                   (y.window, y.start_index, y.coarse, y.fine, y.correction, y.snr)
+        assert np.array_equal(a[s]["fic"], b[s]["fic"]) and np.array_equal(a[s]["crc"], b[s]["crc"])
+        assert sorted(a[s]["msc"]) == sorted(b[s]["msc"]) and len(a[s]["msc"]) > 0
+        assert all(np.array_equal(a[s]["msc"][c], b[s]["msc"][c]) for c in a[s]["msc"])
+        assert sorted(a[s]["soft"]) == sorted(b[s]["soft"])
+        assert all(np.array_equal(a[s]["soft"][g], b[s]["soft"][g]) for g in a[s]["soft"])
 
 
 def _profile_mix():
@@ -271,14 +363,15 @@ def _profile_mix():
     return ens
 
 
-def test_pipeline_every_profile_kind_matches_reference_path(ctx):
+@FMTS
+def test_pipeline_every_profile_kind_matches_reference_path(ctx, fmt):
     """every depuncturing kind through the streaming pipeline at 9 dB (Viterbi decisions
     that matter): MSC bits of every subchannel and the FIC against the reference path"""
     F, runs = 4, 5
     for g, sub in enumerate(_profile_mix()):
-        iqs = _gen(sub, F * runs + 1, [900 + g], 9.0)
+        iqs = _gen(sub, F * runs + 1, [900 + g], 9.0, fmt=fmt)
         ref = orc.decode_stream(iqs[0], F * runs, sub)
-        gpu = pc.gpu_decode(ctx, iqs, F, runs, sub)
+        gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, iq_format=fmt)
         st = pc.compare(gpu[0], ref, sub, check_soft=False)
         print("profiles", g, [s[2:] for s in sub], st)
         _check([st], ("profiles", g), soft=False)

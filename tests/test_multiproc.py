@@ -3,11 +3,12 @@
 Covers what the N-GPU bench relies on: torch.distributed rendezvous from the
 launcher's env vars, the start/stop barrier, the max-over-ranks time, the disjoint
 per-rank ensemble seeds (rank-local mode: each rank decodes its own ensembles) and
-the C4 stream split (--iq-source rccl) through the bench's own code
-(bench.chunk_phases + bench.StreamSplit): rank 0 holds every rank's cyclic int16
-streams and sends each rank chunk k of its OWN ensembles per step; every rank must
-receive exactly its own streams, which must decode (oracle) to its own transmitted
-FIBs, and the per-rank checks gather on every rank."""
+the C4 stream split (the c4_fed leg) through the bench's own code (bench.chunk_phases,
+bench.gather_to_rank0, bench.FedSplit): every rank's recorded streams (u8 .raw and s16
+.sdr) reach rank 0, which sends each rank chunk k of its OWN ensembles into its stream
+buffer per step; every rank must receive exactly its own streams, byte for byte, which
+must decode (oracle) to its own transmitted FIBs, and the per-rank checks gather on
+every rank."""
 import os
 import socket
 import sys
@@ -48,7 +49,7 @@ def _worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def _split_worker(rank, world, port, q):
+def _split_worker(rank, world, port, q, fmt):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "sdr-j-dab_amd")]
@@ -58,29 +59,33 @@ def _split_worker(rank, world, port, q):
     from dabamd.synth import Ensemble
     r, local, w, dist = bench.dist_setup(world)
     E, F = 2, 2
-    ens = Ensemble(7, snr_db=30.0)
+    ens = Ensemble(7, snr_db=30.0, amplitude=bench.AMPLITUDE)
     stride = ens.length
     P = bench.period_frames(F, False)
     cs, nchunks = bench.chunk_layout(stride, F)
-    # the bench's own feed: rank 0 holds every rank's cyclic streams as chunk phases and
-    # sends each rank its own chunk k per step (bench.StreamSplit)
-    src = [torch.from_numpy(bench.chunk_phases(ens, P, cs, E, bench.rank_seed0(d, E), 2)) for d in range(world)] \
-        if rank == 0 else None
-    split = bench.StreamSplit(dist, rank, world, E, cs, P // F, nchunks, "cpu", src)
-    got = np.zeros((E, nchunks * 2 * cs), np.int16)
-    for k in range(nchunks + 1):                          # one call past the end: None
-        chunk = split.end(k, split.begin(k))
-        if k == nchunks:
-            assert chunk is None
-            break
-        got[:, 2 * k * cs:2 * (k + 1) * cs] = chunk.numpy()
     seed0 = bench.rank_seed0(rank, E)
+    # the bench's own C4 feed: every rank's chunk phases reach rank 0 (setup), then rank 0
+    # sends each rank chunk k of its OWN streams straight into that rank's stream buffer
+    mine = torch.from_numpy(bench.chunk_phases(ens, P, cs, E, seed0, 2, fmt))
+    src = bench.gather_to_rank0(dist, rank, world, mine)
+    dt = {"u8": torch.uint8, "s16": torch.int16}[fmt]
+    fiq = torch.zeros((E, 2 * nchunks * cs), dtype=dt)
+    split = bench.FedSplit(dist, rank, world, E, mine.shape[0], src=src,
+                           dst=lambda e, k: fiq[e, 2 * k * cs:2 * (k + 1) * cs])
+    if rank == 0:
+        for k in range(nchunks):
+            fiq[:, 2 * k * cs:2 * (k + 1) * cs].copy_(src[0][k % mine.shape[0]])
+    for k in range(nchunks):
+        split.end(split.begin(k))
+    got = fiq.numpy()
     per = ens.period_many(E, seed0=seed0, period=P, threads=2)
-    mine = np.stack([bench.to_s16(ens.stream_from_period(per[e], P)) for e in range(E)])
-    same = bool(np.array_equal(got[:, :2 * stride], mine))
-    # the received samples decode to this rank's own transmitted bits
+    want = np.stack([bench.to_raw(ens.stream_from_period(per[e], P), fmt) for e in range(E)])
+    same = bool(np.array_equal(got[:, :2 * stride], want))           # byte-identical
+    # the received samples, read back as the format's reader does, decode to this rank's
+    # own transmitted bits
     truth = ens.generate_period(seed0, P, truth=True)
-    iq = got[0, :2 * stride].astype(np.float32) / 32768.0
+    g0 = got[0, :2 * stride]
+    iq = (g0.astype(np.float32) / 32768.0) if fmt == "s16" else ((g0.astype(np.float32) - 128.0) / 128.0)
     ref = orc.decode_stream(iq, 7, [])
     flip = np.zeros(768, np.uint8)
     for b in range(3):
@@ -93,11 +98,12 @@ def _split_worker(rank, world, port, q):
     dist.destroy_process_group()
 
 
-def test_stream_split_scatter_gloo():
+@pytest.mark.parametrize("fmt", ["u8", "s16"])
+def test_stream_split_scatter_gloo(fmt):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q, fmt)) for r in range(2)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
@@ -105,7 +111,7 @@ def test_stream_split_scatter_gloo():
         p.join(timeout=60)
         assert p.exitcode == 0
     (r0, same0, ok0, h0, c0), (r1, same1, ok1, h1, c1) = res
-    assert same0 and same1                   # every rank got exactly its own streams
+    assert same0 and same1                   # every rank got exactly its own streams, byte for byte
     assert ok0 and ok1                       # which decode to its own transmitted FIBs
     assert h0 != h1                          # disjoint ensembles per rank
     assert c0 == c1 == [{"rank": 0, "fic_ok": True}, {"rank": 1, "fic_ok": True}]   # gathered checks

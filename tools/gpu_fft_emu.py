@@ -1,0 +1,81 @@
+"""ANALYSIS TOOL (not test infrastructure, not product): the GPU demod's FFT
+(k_demod.hip fft2048_wg: radix-8 / W2048 twiddles, radix-8 / W256, radix-8 / W32 and the
+quad's DPP radix-4, fma twiddle products) restated in numpy float32, operation for
+operation, so its rounding can be compared with other fp32 transforms on the CPU
+(tools/soft_floor.py).  It reproduces the GPU's soft values (e.g. the max |dq| of
+test_demod_nco_matches_oracle at -4201 Hz, 2.646e-5, to the digit)."""
+import numpy as np
+f32 = np.float32
+W = np.exp(-2j*np.pi*np.arange(2048)/2048)
+Wr = W.real.astype(f32); Wi = W.imag.astype(f32)
+C = f32(0.70710678118654752440)
+def fmaf(a,b,c):  # float32 fma emulated in double (product exact)
+    return (a.astype(np.float64)*b.astype(np.float64) + c.astype(np.float64)).astype(f32)
+def cmul(ar, ai, wr, wi):
+    return fmaf(ar, wr, -(ai*wi)), fmaf(ar, wi, ai*wr)
+def dft8(ar, ai):  # ar, ai: lists of 8 arrays
+    br=[None]*8; bi=[None]*8
+    for j in range(4):
+        br[j]=ar[j]+ar[j+4]; bi[j]=ai[j]+ai[j+4]
+        br[j+4]=ar[j]-ar[j+4]; bi[j+4]=ai[j]-ai[j+4]
+    br[5], bi[5] = C*(br[5]+bi[5]), C*(bi[5]-br[5])
+    br[6], bi[6] = bi[6], -br[6]
+    br[7], bi[7] = C*(bi[7]-br[7]), -C*(br[7]+bi[7])
+    dr=[None]*8; di=[None]*8
+    for h in (0,4):
+        dr[h]=br[h]+br[h+2]; di[h]=bi[h]+bi[h+2]
+        dr[h+1]=br[h+1]+br[h+3]; di[h+1]=bi[h+1]+bi[h+3]
+        dr[h+2]=br[h]-br[h+2]; di[h+2]=bi[h]-bi[h+2]
+        tr=br[h+1]-br[h+3]; ti=bi[h+1]-bi[h+3]
+        dr[h+3]=ti; di[h+3]=-tr
+    o_r=[None]*8; o_i=[None]*8
+    pairs=[(0,4,0,1),(2,6,2,3),(1,5,4,5),(3,7,6,7)]
+    for a,b,x,y in pairs:
+        o_r[a]=dr[x]+dr[y]; o_i[a]=di[x]+di[y]
+        o_r[b]=dr[x]-dr[y]; o_i[b]=di[x]-di[y]
+    return o_r, o_i
+def gpu_fft(x):
+    """x: complex64 [..., 2048] -> complex64 X as fft2048_wg computes it"""
+    xr = x.real.astype(f32); xi = x.imag.astype(f32)
+    sh = x.shape[:-1]
+    t = np.arange(256)
+    # pass 1
+    ar=[xr[..., t+256*m] for m in range(8)]; ai=[xi[..., t+256*m] for m in range(8)]
+    ar, ai = dft8(ar, ai)
+    for k in range(1,8):
+        ar[k], ai[k] = cmul(ar[k], ai[k], Wr[(t*k)&2047], Wi[(t*k)&2047])
+    exr = np.empty(sh+(2048,), f32); exi = np.empty(sh+(2048,), f32)
+    for k in range(8):
+        exr[..., k*256+t]=ar[k]; exi[..., k*256+t]=ai[k]
+    # pass 2
+    k1 = t>>5; tp = t&31
+    ar=[exr[..., k1*256+tp+32*m] for m in range(8)]; ai=[exi[..., k1*256+tp+32*m] for m in range(8)]
+    ar, ai = dft8(ar, ai)
+    for k in range(1,8):
+        ar[k], ai[k] = cmul(ar[k], ai[k], Wr[(8*(tp*k))&2047], Wi[(8*(tp*k))&2047])
+    ex2r = np.empty(sh+(2048,), f32); ex2i = np.empty(sh+(2048,), f32)
+    for k in range(8):
+        ex2r[..., (k1*8+k)*32+tp]=ar[k]; ex2i[..., (k1*8+k)*32+tp]=ai[k]
+    # pass 3
+    g = t>>2; tq = t&3
+    ar=[ex2r[..., g*32+tq+4*m] for m in range(8)]; ai=[ex2i[..., g*32+tq+4*m] for m in range(8)]
+    ar, ai = dft8(ar, ai)
+    for k in range(1,8):
+        wr = np.where(tq>0, Wr[(64*(tq*k))&2047], f32(1)); wi = np.where(tq>0, Wi[(64*(tq*k))&2047], f32(0))
+        nr, ni = cmul(ar[k], ai[k], wr, wi)
+        ar[k] = np.where(tq>0, nr, ar[k]); ai[k] = np.where(tq>0, ni, ai[k])
+    # pass 4: radix-4 across quads (lanes t: partner t^2 then t^1)
+    def bfly(v, M):
+        idx = t ^ M
+        p = v[..., idx]
+        sign = np.where(t & M, f32(-1), f32(1))
+        return fmaf(sign, v, p)
+    out = np.empty(sh+(2048,), np.complex64)
+    b0 = (g>>3) + 8*(g&7) + 512*(((tq&1)<<1)|(tq>>1))
+    for k in range(8):
+        vr = bfly(ar[k], 2); vi = bfly(ai[k], 2)
+        rot = tq == 3
+        vr, vi = np.where(rot, vi, vr), np.where(rot, -vr, vi)
+        vr = bfly(vr, 1); vi = bfly(vi, 1)
+        out[..., b0 + 64*k] = vr + 1j*vi
+    return out
