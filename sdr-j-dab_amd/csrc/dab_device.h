@@ -56,28 +56,43 @@ __device__ __forceinline__ float2 nco_value(const double2 *tab, int32_t t) {
 //   F32  interleaved cf32 as virtualInput::getSamples hands it over
 //   S16  .sdr PCM16 (wavfiles.cpp:172, sf_readf_float: x / 32768)
 //   U8   .raw (rawfiles.cpp:115-117: float(x - 128) / 128.0 = x / 128 - 1)
-// raw: what a prefetch register holds (8, 4 or 2 bytes per sample); bps: bytes per sample
+// raw: what a prefetch register holds (8, 4 or 2 bytes per sample); bps: bytes per sample.
+// cvt: the sample as the reader hands it over; scaled: the same times 2^scale_exp (the
+// integer the file holds, one instruction less per value: the demod keeps its samples,
+// spectra and FreqCorr scaled by that power of two -- every float rounding commutes with it
+// -- and unscales only what leaves it in absolute units); unscale = 2^-scale_exp.
 template <int FMT> struct IqFmt;
 template <> struct IqFmt<DABGPU_IQ_F32> {
     typedef float2 raw;
     static constexpr int bps = 8;
+    static constexpr float unscale = 1.0f;
     __device__ static raw load(__amdgpu_buffer_rsrc_t r, int32_t off) {
         return __builtin_bit_cast(float2, __builtin_amdgcn_raw_buffer_load_b64(r, off, 0, 0));
     }
     __device__ static float2 cvt(raw v) { return v; }
+    __device__ static float2 scaled(raw v) { return v; }
 };
 template <> struct IqFmt<DABGPU_IQ_S16> {
     typedef uint32_t raw;
     static constexpr int bps = 4;
+    static constexpr float unscale = 0x1p-15f;
     __device__ static raw load(__amdgpu_buffer_rsrc_t r, int32_t off) { return __builtin_amdgcn_raw_buffer_load_b32(r, off, 0, 0); }
+    __device__ static float2 scaled(raw v) {
+        return make_float2((float)(int32_t)(int16_t)(v & 0xFFFFu), (float)((int32_t)v >> 16));
+    }
     __device__ static float2 cvt(raw v) {
-        return make_float2((float)(int32_t)(int16_t)(v & 0xFFFFu) * 0x1p-15f, (float)((int32_t)v >> 16) * 0x1p-15f);
+        const float2 s = scaled(v);
+        return make_float2(s.x * unscale, s.y * unscale);
     }
 };
 template <> struct IqFmt<DABGPU_IQ_U8> {
     typedef uint32_t raw;
     static constexpr int bps = 2;
+    static constexpr float unscale = 0x1p-7f;
     __device__ static raw load(__amdgpu_buffer_rsrc_t r, int32_t off) { return __builtin_amdgcn_raw_buffer_load_b16(r, off, 0, 0); }
+    __device__ static float2 scaled(raw v) {        // x - 128 (exact)
+        return make_float2((float)(v & 0xFFu) - 128.0f, (float)((v >> 8) & 0xFFu) - 128.0f);
+    }
     __device__ static float2 cvt(raw v) {
         // (float)(x - 128) / 128 == x * 2^-7 - 1 exactly (x < 256): one fma per value
         return make_float2(__builtin_fmaf((float)(v & 0xFFu), 0x1p-7f, -1.0f), __builtin_fmaf((float)((v >> 8) & 0xFFu), 0x1p-7f, -1.0f));

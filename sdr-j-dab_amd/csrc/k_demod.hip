@@ -289,13 +289,13 @@ __device__ __forceinline__ int32_t prs_corr_wg(float2 (&a)[8], float2 *ex, const
 // (dab-constants.h:107-109).  The sums are workgroup trees (the reference adds in bin
 // order): a display value, equal to the sequential one except within float rounding
 // of a dB boundary.
-__device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R) {
+__device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R, float unscale = 1.0f) {
     const int b0 = bin0_of(t);
     float noise = 0.0f, signal = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
         const int b = b0 + 64 * k;
-        const float v = hypotf(a[k].x, a[k].y);
+        const float v = hypotf(a[k].x * unscale, a[k].y * unscale);      // (a power of two: exact)
         if ((b >= 1034 && b < 1260) || (b >= 788 && b < 1014)) noise += v;
         if (b >= 1664 || b < 384) signal += v;
     }
@@ -457,7 +457,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
             const int32_t o = ((l0 - 1) * TS + t) * BPS;
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = Fmt::cvt(ld(o + 256 * BPS * m));
+            for (int m = 0; m < 8; m++) a[m] = Fmt::scaled(ld(o + 256 * BPS * m));
             if (l0 == 1) mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
             else mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
         }
@@ -468,7 +468,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
         for (int m = 0; m < 8; m++) nx[m] = ld(ov + 256 * BPS * m);
         fft2048_wg(a, ex, tw, t);
         if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
-            const int16_t v = snr_wg(a, t, red);
+            const int16_t v = snr_wg(a, t, red, Fmt::unscale);
             if (t == 0) aux.snr[fi] = v;
         }
         __syncthreads();                                // pass 3 read ex: the first symbol's pass 1 writes it
@@ -505,14 +505,15 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
             const double2 d = nco_value_d(ncl, nco_mod(-(int64_t)dsym));
             rr = uni(r.x); ri = uni(r.y);
             dr = uni(d.x); di = uni(d.y);
+
             efc = nco_value(ncl, nco_mod(-(int64_t)TU * ph));
         }
         for (int l = l0; l < l1; l++) {
             // this symbol's samples and its guard samples, all loaded one symbol ahead
             // (a guard load issued here would expose a full HBM latency per symbol)
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = Fmt::cvt(nx[m]);
-            const float2 g6 = Fmt::cvt(ng6), g7 = Fmt::cvt(ng7);
+            for (int m = 0; m < 8; m++) a[m] = Fmt::scaled(nx[m]);
+            const float2 g6 = Fmt::scaled(ng6), g7 = Fmt::scaled(ng7);
             if (l + 1 < l1) {
                 const int32_t o1 = ov + TS * BPS;
                 ng6 = ld(o1 - 512 * BPS);
@@ -556,8 +557,9 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const int b = b0 + 64 * k;
-                    if (b < K / 2) dp[b] = a[k];
-                    else if (b >= TU - 1 - K / 2 && b < TU - 1) dp[b - (TU - 1 - K)] = a[k];
+                    const float2 v = make_float2(a[k].x * Fmt::unscale, a[k].y * Fmt::unscale);
+                    if (b < K / 2) dp[b] = v;
+                    else if (b >= TU - 1 - K / 2 && b < TU - 1) dp[b - (TU - 1 - K)] = v;
                 }
             }
             __syncthreads();                           // pass 3's reads of ex done: st reuses it
@@ -640,6 +642,8 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
             __syncthreads();
         }
         fc = cmulw(fc, efc);
+        fc.x *= Fmt::unscale * Fmt::unscale;           // the partial sums in absolute units (exact)
+        fc.y *= Fmt::unscale * Fmt::unscale;
     }
     fc.x = wave_sum(fc.x);
     fc.y = wave_sum(fc.y);

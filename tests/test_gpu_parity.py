@@ -275,18 +275,18 @@ def _nco_mix(x, pos, lp, phase, origin, osc):
     return np.stack([re, im], axis=1).astype(np.float32)
 
 
-def _cfo_frames(cfo, nframes=4, seed=29, phase_b_off=17):
+def _cfo_frames(cfo, nframes=4, seed=29, phase_b_off=17, nco=None):
     """a stream transmitted cfo Hz off, its frames as the oracle's ofdmProcessor::run
-    places them (settled windows), demodulated with phase_a = round(cfo) over the sync
-    window and block 0 and phase_b = phase_a + phase_b_off over the data symbols, at
-    arbitrary localPhase offsets"""
+    places them (settled windows), demodulated with phase_a = round(cfo) (or `nco`) over
+    the sync window and block 0 and phase_b = phase_a + phase_b_off over the data
+    symbols, at arbitrary localPhase offsets"""
     import dabamd
     from dabamd.synth import Ensemble
     g = Ensemble(nframes, subch=[(0, 96, 128, 3, 1, 0)], snr_db=12.0, cfo_hz=cfo).generate(seed, truth=False)
     n, info, _ = orc.ofdm_run(g["iq"], nframes)
     assert n >= 3
     info = info[1:n]                                  # frames with a settled window
-    phase = int(round(cfo))
+    phase = int(round(cfo)) if nco is None else nco
     x = g["iq"].reshape(-1, 2)
     frs = []
     for i, fi in enumerate(info):
@@ -297,13 +297,21 @@ def _cfo_frames(cfo, nframes=4, seed=29, phase_b_off=17):
     return g, x, frs
 
 
-# the five carrier offsets of the NCO parity cases: the stream
-# transmitted cfo Hz off, corrected by phase_a = round(cfo) and phase_b = phase_a + 17
-NCO_CFOS = [1300.0, -4201.0, 517.0, 7333.0, 12345.0]
+# the NCO parity cases: (transmitted offset, NCO phase) -- the
+# stream transmitted cfo Hz off, corrected by phase_a = round(cfo), phase_b = phase_a + 17;
+# the last: a 0 Hz stream through a 12345 Hz NCO in both segments (every carrier 12.3
+# bins off, smeared -- the receiver before its coarse AFC locks: round 4's failing
+# 12345 Hz configuration, gpurun_out/r04c/t_*.log)
+NCO_CASES = [(1300.0, None), (-4201.0, None), (517.0, None), (7333.0, None), (12345.0, None), (0.0, 12345)]
 
 
-@pytest.mark.parametrize("cfo", NCO_CFOS)
-def test_demod_nco_matches_oracle(ctx, cfo):
+def _case_off(nco):
+    return 17 if nco is None else 0
+NCO_CFOS = [c for c, _ in NCO_CASES]
+
+
+@pytest.mark.parametrize("cfo,nco", NCO_CASES, ids=["1300", "-4201", "517", "7333", "12345", "0-nco12345"])
+def test_demod_nco_matches_oracle(ctx, cfo, nco):
     """processToken under a carrier offset, through the per-sample NCO of getSamples
     (ofdm-processor.cpp:186-201): the GPU demod's float soft values against the
     oracle's on the reference-mixed samples, UNWEIGHTED max |q_gpu - q_oracle| <=
@@ -321,7 +329,7 @@ def test_demod_nco_matches_oracle(ctx, cfo):
     NCO segments).  int16 soft bits equal except at rounding boundaries; FreqCorr
     (ofdm-processor.cpp:424-438) within 1e-3."""
     import dabamd
-    g, x, frs = _cfo_frames(cfo)
+    g, x, frs = _cfo_frames(cfo, nco=nco, phase_b_off=_case_off(nco))
     osc = dabamd.host_table(dabamd.TABLE_OSC)
     iq = ctx.put(g["iq"])
     soft, softf, fc = ctx.demod(iq, frs, with_float=True)
@@ -361,7 +369,7 @@ def test_demod_nco_matches_oracle(ctx, cfo):
         assert abs(fc[i] - fc_ref) <= 1e-3 * abs(fc_ref) + 1e-3, (cfo, i, fc[i], fc_ref)
     iq.free()
     floor = max(floor32.values())
-    print(f"cfo {cfo}: max |q_gpu - q_oracle| {worst:.3e} (unweighted); fp32 floor {floor:.3e} ("
+    print(f"cfo {cfo} nco {nco}: max |q_gpu - q_oracle| {worst:.3e} (unweighted); fp32 floor {floor:.3e} ("
           + ", ".join(f"{kinds[k]} {v:.3e}" for k, v in floor32.items())
           + f"); weighted by min(1, |r| / rms|r|) {worst_c:.3e}")
     assert worst <= max(SOFT_TOL, floor), (cfo, worst, floor32, worst_c)

@@ -1,5 +1,5 @@
-"""The soft values' fp32 floor, on the CPU: for the five carrier
-offsets of test_demod_nco_matches_oracle (the same streams, frames and NCO-mixed samples),
+"""The soft values' fp32 floor, on the CPU: for the six cases
+(transmitted offset / NCO phase) of test_demod_nco_matches_oracle (the same streams, frames and NCO-mixed samples),
 max |q - q_oracle| over every soft value of 3 frames x 75 symbols when the FFT is
   gpu-emu      the GPU demod's radix-8/8/8/4 transform (tools/gpu_fft_emu.py)
   radix-4      the oracle's fp32 radix-4 Stockham transform (orc_fft2048_f32)
@@ -17,7 +17,7 @@ sys.path[:0] = [os.path.join(ROOT, "sdr-j-dab_amd"), os.path.join(ROOT, "tests")
 import dabamd                                    # noqa: E402
 import gpu_fft_emu                               # noqa: E402
 import oracle_py as orc                          # noqa: E402
-from test_gpu_parity import NCO_CFOS, _cfo_frames, _nco_mix   # noqa: E402
+from test_gpu_parity import NCO_CASES, _case_off, _cfo_frames, _nco_mix   # noqa: E402
 
 osc = dabamd.host_table(dabamd.TABLE_OSC)
 mp = dabamd.host_table(dabamd.TABLE_MAPPER).astype(np.int64)
@@ -48,10 +48,12 @@ def main():
     print(f"  gpu-emu {rel(gpu_fft_emu.gpu_fft(x)):.3e}   double->f32 {rel(ffts(x, 0)):.3e}   " +
           "   ".join(f"{k} {rel(ffts(x, v)):.3e}" for k, v in KINDS.items()))
     print()
-    print("max |q - q_oracle| (unweighted) per case, and [soft values off by > 1e-5]:")
-    print(f"  {'cfo':>8} " + " ".join(f"{k:>20}" for k in ["gpu-emu"] + list(KINDS)))
-    for cfo in NCO_CFOS:
-        g, xs, frs = _cfo_frames(cfo)
+    print("max |q - q_oracle| (unweighted) per case (transmitted offset / NCO phase + data-symbol phase offset),")
+    print("and [soft values off by > 1e-5]; the last row is the smeared case with the +17 data offset (not a test case):")
+    print(f"  {'cfo/nco':>14} " + " ".join(f"{k:>20}" for k in ["gpu-emu"] + list(KINDS)))
+    cases = [(c, n, _case_off(n)) for c, n in NCO_CASES] + [(0.0, 12345, 17)]
+    for cfo, nco, off in cases:
+        g, xs, frs = _cfo_frames(cfo, nco=nco, phase_b_off=off)
         res = {k: [0.0, 0] for k in ["gpu-emu"] + list(KINDS)}
         for fr in frs:
             pa = np.arange(fr.block0, fr.block0 + 2048)
@@ -71,7 +73,7 @@ def main():
                     d = np.abs(q_of(X[l], X[l - 1]) - qd)
                     res[k][0] = max(res[k][0], float(d.max()))
                     res[k][1] += int((d > 1e-5).sum())
-        print(f"  {cfo:8.0f} " + " ".join(f"{v[0]:11.3e} [{v[1]:5d}]" for v in res.values()))
+        print(f"  {cfo:6.0f}/{nco if nco is not None else round(cfo):6.0f}+{off:<2d}" + " ".join(f"{v[0]:11.3e} [{v[1]:5d}]" for v in res.values()))
 
 
 if __name__ == "__main__":
