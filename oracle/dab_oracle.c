@@ -772,7 +772,7 @@ notSynced:
             if (dst) memcpy(dst + (l - 1) * 2 * ORC_K, ibits, sizeof ibits);
             /* the IQ display (ofdm-decoder.cpp:192-206): every 8th displayToken (2) the
              * carriers fft_buffer[0, K/2) and [T_u - 1 - K/2, T_u - 1) into iqBuffer */
-            if (l == 2 && ++iq_cnt > 7) {
+            if (l == (disp && disp->token ? disp->token : 2) && ++iq_cnt > 7) {
                 if (disp && disp->n_disp < disp->max_disp) {
                     float *o = disp->iq_disp + (int64_t)disp->n_disp * 2 * ORC_K;
                     memcpy(o, X, sizeof(float) * ORC_K);

@@ -100,6 +100,7 @@ typedef struct {
     int32_t  max_disp, n_disp;
     int64_t *spec_start;    /* [max_spec] */
     int32_t  max_spec, n_spec;
+    int32_t  token;         /* displayToken (ofdm-decoder.cpp:61; 0 means the reference's 2) */
 } orc_display;
 int     orc_ofdm_run_display(const float *iq, int64_t n, int16_t threshold, int method, int max_frames,
                              orc_frame_info *info, int16_t *softbits, orc_display *disp);

@@ -101,6 +101,8 @@ def lib() -> C.CDLL:
             "dabgpu_nco_eval": ([vp, i32, i32, vp], i32),
             "dabgpu_ofdm_demod_mix": ([vp, vp, vp, i32, i32, vp, vp], i32),
             "dabgpu_pipe_set_iq_format": ([vp, i32], i32),
+            "dabgpu_pipe_acquire_wait": ([vp], i32),
+            "dabgpu_pipe_set_display_token": ([vp, i32], i32),
             "dabgpu_iq_convert": ([vp, i32, vp, i64, vp], i32),
             "dabgpu_event_record": ([vp, i32], i32),
             "dabgpu_kernel_errors": ([vp], i32),
@@ -663,6 +665,14 @@ class Pipeline:
         msc [S, 4F, n_subch, msc_stride_packed] bytes"""
         _chk(lib().dabgpu_pipe_set_packed(self.h, int(on)), "dabgpu_pipe_set_packed")
         self.packed = bool(on)
+
+    def acquire_wait(self) -> None:
+        """wait for a background null search in flight and apply it (dabgpu_pipe_acquire_wait)"""
+        _chk(lib().dabgpu_pipe_acquire_wait(self.h), "dabgpu_pipe_acquire_wait")
+
+    def set_display_token(self, token: int) -> None:
+        """the symbol (1..75) the display feed keeps (ofdmDecoder::set_displayToken)"""
+        _chk(lib().dabgpu_pipe_set_display_token(self.h, int(token)), "dabgpu_pipe_set_display_token")
 
     def set_iq_format(self, fmt: int) -> None:
         """sample format of the streams acquire() / run() read: IQ_F32 (default), IQ_S16

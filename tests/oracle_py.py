@@ -94,10 +94,10 @@ def ofdm_run(iq, max_frames, threshold=3, method=1, fft_kind=0):
 
 class Display(C.Structure):
     _fields_ = [("iq_disp", C.c_void_p), ("disp_frame", C.c_void_p), ("max_disp", C.c_int32), ("n_disp", C.c_int32),
-                ("spec_start", C.c_void_p), ("max_spec", C.c_int32), ("n_spec", C.c_int32)]
+                ("spec_start", C.c_void_p), ("max_spec", C.c_int32), ("n_spec", C.c_int32), ("token", C.c_int32)]
 
 
-def ofdm_run_display(iq, max_frames, threshold=3, method=1, max_disp=64, max_spec=64):
+def ofdm_run_display(iq, max_frames, threshold=3, method=1, max_disp=64, max_spec=64, token=2):
     """ofdm_run plus the reference's display feeds: (n, info, soft, iq_disp [k][1536] complex64,
     disp_frame [k], spec_start [k]) -- iqBuffer (ofdm-decoder.cpp:192-206) and
     spectrumBuffer (ofdm-processor.cpp:161-180,220-238) emissions in order"""
@@ -106,7 +106,7 @@ def ofdm_run_display(iq, max_frames, threshold=3, method=1, max_disp=64, max_spe
     disp = np.zeros((max_disp, 1536, 2), np.float32)
     dfr = np.zeros(max_disp, np.int32)
     spec = np.zeros(max_spec, np.int64)
-    d = Display(disp.ctypes.data, dfr.ctypes.data, max_disp, 0, spec.ctypes.data, max_spec, 0)
+    d = Display(disp.ctypes.data, dfr.ctypes.data, max_disp, 0, spec.ctypes.data, max_spec, 0, token)
     n = oracle().orc_ofdm_run_display(P(iq), C.c_int64(len(iq) // 2), C.c_int16(threshold), method, max_frames, info,
                                       P(soft), C.byref(d))
     nd, ns = min(d.n_disp, max_disp), min(d.n_spec, max_spec)

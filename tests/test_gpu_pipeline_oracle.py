@@ -210,7 +210,7 @@ def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
     runs0 = [(x.frames_run, x.acquiring, x.resyncs) for x in gpu[0]["states"]]
     print("background re-acquisition:", runs0)
     assert all(x.frames_run == F for x in gpu[1]["states"])          # stream 1 never waits
-    assert any(fr < F for fr, _, _ in runs0) and any(acq for _, acq, _ in runs0)
+    assert any(fr < F for fr, _, _ in runs0)                          # stream 0 missed runs while searching
     assert gpu[0]["states"][-1].resyncs >= 1 and gpu[0]["states"][-1].acquisitions >= 2
     for s in range(2):
         st = pc.compare(gpu[s], refs[s], sub)
@@ -218,6 +218,63 @@ def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
         _check([st], ("background", s))
     st0 = pc.compare(gpu[0], refs[0], sub)
     assert st0["frames"] > 4                   # frames after the dropout were decoded too
+
+
+def test_background_search_flag_clears_without_a_run(ctx):
+    """dabgpu_stream_state.acquiring tells a caller when the background null
+    search (DABGPU_CTL_ACQ_ASYNC) no longer reads iq_d -- it clears once the search is done,
+    seen through dabgpu_pipe_state alone (no further run); dabgpu_pipe_acquire_wait waits
+    for it; a RESYNC issued while a search is in flight waits for it and wins (the stream
+    searches again from its new position at the next run)"""
+    import time
+    import dabamd
+    from dabamd.synth import Ensemble
+    sub = MIXED[:1]
+    F = 4
+    e = Ensemble(6 * F + 4, subch=sub, snr_db=20.0)
+    g = e.generate(51, truth=False)
+    iq = g["iq"].reshape(-1, 2).copy()
+    a = g["frame0"] + 3 * 196608 + 40000
+    b = a + 300000
+    level = float(np.sqrt((iq[:200000] ** 2).sum(1).mean()))
+    ph = 2 * np.pi * 100e3 / 2048000 * np.arange(b - a)
+    iq[a:b, 0] = level * np.cos(ph)
+    iq[a:b, 1] = level * np.sin(ph)
+    x = np.ascontiguousarray(iq.reshape(-1))
+    n = len(x) // 2
+    diq = ctx.put(x[None, :])
+
+    def until_loss(pipe):
+        pipe.acquire(diq, n, [0], [n])
+        pipe.control(dabamd.CTL_ACQ_ASYNC)
+        for r in range(5):
+            pipe.run(diq, n, [n], partial=True)
+            if pipe.state(0).frames_run < F:          # the sync loss: a search was launched
+                return True
+        return False
+    try:
+        for mode in ("poll", "resync"):
+            pipe = dabamd.Pipeline(ctx, 1, F, [dabamd.Subch(*sub[0][:4], 0, 0)])
+            try:
+                assert until_loss(pipe)
+                if mode == "poll":
+                    t0 = time.time()
+                    while pipe.state(0).acquiring and time.time() - t0 < 5.0:
+                        time.sleep(0.001)
+                    assert pipe.state(0).acquiring == 0        # cleared without another run
+                    pipe.acquire_wait()                         # nothing in flight: at once
+                else:
+                    pipe.control(dabamd.CTL_RESYNC)             # at once: the search may be in flight
+                    st = pipe.state(0)
+                    assert st.acquiring == 0 and st.synced == 0  # it waited, and RESYNC won
+                pipe.run(diq, n, [n], partial=True)             # decodes on from there
+                pipe.acquire_wait()
+                pipe.sync()
+                ctx.check()
+            finally:
+                pipe.close()
+    finally:
+        diq.free()
 
 
 @FMTS
@@ -525,23 +582,27 @@ def test_null_search_matches_reference_on_random_streams(ctx, scan):
         diq.free()
 
 
-def test_pipeline_iq_display_matches_reference_feed(ctx):
+@pytest.mark.parametrize("token", [2, 5])
+def test_pipeline_iq_display_matches_reference_feed(ctx, token):
     """the constellation feed (ofdmDecoder::processToken, ofdm-decoder.cpp:192-206): the
-    pipeline's symbol-2 display carriers of every 8th frame equal the oracle's iqBuffer
+    pipeline's display-token carriers of every 8th frame equal the oracle's iqBuffer
     pushes (fft_buffer[0, K/2) and [T_u-1-K/2, T_u-1) of the same frame) within 1e-5 of
-    the spectrum's RMS, under a carrier offset (the NCO-mixed samples' FFT)"""
+    the spectrum's RMS, under a carrier offset (the NCO-mixed samples' FFT); token 5 via
+    set_displayToken (ofdm-decoder.h:50; dabgpu_pipe_set_display_token)"""
     import dabamd
     from dabamd.synth import Ensemble
     F, runs = 8, 2
     sub = [(0, 96, 128, 3, 1)]
     e = Ensemble(F * runs + 1, subch=[s + (0,) for s in sub], snr_db=20.0, cfo_hz=1300.0)
     iq = e.generate(55, truth=False)["iq"]
-    n, info, _, disp, dfr, _ = orc.ofdm_run_display(iq, F * runs)
+    n, info, _, disp, dfr, _ = orc.ofdm_run_display(iq, F * runs, token=token)
     assert n == F * runs and list(dfr) == [7, 15]
     diq = ctx.put(iq[None, :])
     subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, 0) for s in sub]
     pipe = dabamd.Pipeline(ctx, 1, F, subs)
     pipe.set_display(True)
+    if token != 2:
+        pipe.set_display_token(token)
     got = {}
     try:
         for r in range(runs):
@@ -565,23 +626,40 @@ def test_pipeline_back_end_bounds_error_reported_once(ctx):
     """the back-end streams' error path: an MSC job handed a subchannel offset
     past the soft-bit ring (DABGPU_CTL_INJECT_BOUNDS) is refused by the Viterbi loader; the
     pipeline reports DABGPU_E_BOUNDS exactly once (at dabgpu_pipe_sync), and the next run
-    and sync succeed with correct FIC/MSC bits"""
+    and sync succeed with correct FIC/MSC bits.  The refused subchannel is decoded from
+    erasures (the RING8 loader substitutes the erasure byte 127 where the int16
+    form reads 0), i.e. exactly the reference's Viterbi of an all-zero soft block, and the
+    other subchannel of the same run is unaffected"""
     import dabamd
     sub = MIXED[:2]
     F = 2
-    iqs = _gen(sub, 3 * F + 1, [71], 30.0)
-    ref = orc.decode_stream(iqs[0], 3 * F, sub)
+    iqs = _gen(sub, 5 * F + 1, [71], 30.0)
+    ref = orc.decode_stream(iqs[0], 5 * F, sub)
     diq = ctx.put(iqs[0][None, :])
     subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, 0) for s in sub]
     pipe = dabamd.Pipeline(ctx, 1, F, subs)
     n = len(iqs[0]) // 2
     try:
-        pipe.run(diq, n, [n])                          # clean
+        for _ in range(3):                             # clean, past the 16-CIF warm-up
+            pipe.run(diq, n, [n])
         pipe.control(dabamd.CTL_INJECT_BOUNDS)
-        pipe.run(diq, n, [n], download=False)          # the faulty back end runs behind this call
+        valid1 = pipe.run(diq, n, [n], download=False)  # the faulty back end runs behind this call
         with pytest.raises(dabamd.DabError, match="out-of-bounds"):
             pipe.sync()
         pipe.sync()                                    # reported once
+        st = pipe.state(0)
+        cif0 = st.cif_count - 4 * st.frames_run
+        msc1 = pipe.msc_d.download(np.uint8, (1, 4 * F, len(sub), pipe.msc_stride))
+        nb0 = 24 * sub[0][2]
+        erased = orc.viterbi(np.zeros(4 * (nb0 + 6), np.int16), nb0) ^ orc.prbs(nb0)
+        nvalid = 0
+        for c in range(4 * F):
+            if valid1[0, c]:
+                nvalid += 1
+                assert np.array_equal(msc1[0, c, 0, :nb0], erased)                  # refused: erasures
+                nb1 = 24 * sub[1][2]
+                assert np.array_equal(msc1[0, c, 1, :nb1], ref["msc"][cif0 + c, 1, :nb1])
+        assert nvalid > 0
         fic, crc, msc, valid = pipe.run(diq, n, [n])   # and the pipeline goes on
         pipe.sync()
         st = pipe.state(0)
