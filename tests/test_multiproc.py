@@ -98,23 +98,24 @@ def _split_worker(rank, world, port, q, fmt):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("fmt", ["u8", "s16"])
-def test_stream_split_scatter_gloo(fmt):
+@pytest.mark.parametrize("fmt,world", [("u8", 2), ("s16", 2), ("u8", 3)])
+def test_stream_split_scatter_gloo(fmt, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_split_worker, args=(r, 2, port, q, fmt)) for r in range(2)]
+    procs = [ctx.Process(target=_split_worker, args=(r, world, port, q, fmt)) for r in range(world)]
     for p in procs:
         p.start()
     res = sorted(q.get(timeout=240) for _ in procs)
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0
-    (r0, same0, ok0, h0, c0), (r1, same1, ok1, h1, c1) = res
-    assert same0 and same1                   # every rank got exactly its own streams, byte for byte
-    assert ok0 and ok1                       # which decode to its own transmitted FIBs
-    assert h0 != h1                          # disjoint ensembles per rank
-    assert c0 == c1 == [{"rank": 0, "fic_ok": True}, {"rank": 1, "fic_ok": True}]   # gathered checks
+    want = [{"rank": r, "fic_ok": True} for r in range(world)]
+    for r, same, ok, h, checks in res:
+        assert same                          # every rank got exactly its own streams, byte for byte
+        assert ok                            # which decode to its own transmitted FIBs
+        assert checks == want                # gathered checks, on every rank
+    assert len({h for _, _, _, h, _ in res}) == world    # disjoint ensembles per rank
 
 
 def test_two_ranks_gloo():
