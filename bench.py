@@ -550,8 +550,10 @@ def main():
         n = min(8, E - g0)
         per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
         for e in range(n):
+            raw = to_raw(per[e], args.iq_format)          # once per period, not per repeated piece
             for p, q, m in ens.stream_pieces(P):
-                diq.upload_at(to_raw(per[e, 2 * q:2 * (q + m)], args.iq_format), ((g0 + e) * stride + p) * bps)
+                diq.upload_at(raw[2 * q:2 * (q + m)], ((g0 + e) * stride + p) * bps)
+            del raw
         if fed:
             fill_chunk_phases(fed_ph, per, ens, P, cs, g0, args.fed_format)
         del per

@@ -594,7 +594,10 @@ int dabgpu_block0(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n,
 // rounds of resident workgroups (kDemodWgPerCu per CU) cost least:
 // rounds * (symbols per chunk + 1 warm-up symbol).
 static const int kMaxChunks = 25;
-static const int kDemodWgPerCu = 3;
+#ifndef DEMOD_CHUNK_WG_PER_CU
+#define DEMOD_CHUNK_WG_PER_CU 3
+#endif
+static const int kDemodWgPerCu = DEMOD_CHUNK_WG_PER_CU;
 static int num_cus() {
     static int cus = 0;
     if (!cus) {

@@ -99,7 +99,9 @@ __device__ __forceinline__ void dft8(float2 (&a)[8]) {
 template <int M>
 __device__ __forceinline__ float quad_bfly(float v, float sign) {
     constexpr int ctrl = M == 2 ? 0x4E : 0xB1;          // quad_perm [2,3,0,1] / [1,0,3,2]
-    const float p = __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), ctrl, 0xF, 0xF, false));
+    // every quad_perm source lane exists: bound_ctrl with full masks, so no old value
+    // (a zeroed destination per move) is needed
+    const float p = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), ctrl, 0xF, 0xF, true));
     return fmaf(sign, v, p);
 }
 
@@ -566,7 +568,8 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
             // DQPSK + soft bits of the 8 bins, fast path first; the few bins whose
             // truncation the fast path cannot decide (soft_fast) are redone exactly after
             // all 8 (one divergent branch per symbol instead of one per bin)
-            uint32_t risky = 0;
+            // (the flag is a lane mask in SGPRs: the rare lanes recompute which bins need it)
+            bool risky = false;
 #pragma unroll
             for (int k = 0; k < 8; k++) {
                 const float2 r1 = cmul_conj_exact(a[k], P[k]);
@@ -574,16 +577,17 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
                 // ab1 = |re| + |im| (ofdm-decoder.cpp:185-189)
                 const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                 int ir, ii;
-                risky |= (uint32_t)soft_fast(r1, ab1, ir, ii) << k;
+                risky |= soft_fast(r1, ab1, ir, ii);
                 const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
                 *(uint32_t *)((char *)st + addr) = spair(ir, ii);
             }
             if (risky) {
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
-                    if ((risky >> k) & 1u) {
-                        const float2 r1 = cmul_conj_exact(a[k], P[k]);
-                        const float ab1 = fabsf(r1.x) + fabsf(r1.y);
+                    const float2 r1 = cmul_conj_exact(a[k], P[k]);
+                    const float ab1 = fabsf(r1.x) + fabsf(r1.y);
+                    int ir, ii;
+                    if (soft_fast(r1, ab1, ir, ii)) {
                         const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
                         *(uint32_t *)((char *)st + addr) = spair(trunc127d(-r1.x / ab1), trunc127d(-r1.y / ab1));
                     }
