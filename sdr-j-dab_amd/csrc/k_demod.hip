@@ -317,17 +317,26 @@ __device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R
 // truncation (v_cvt_i32_f32 truncates) equals the reference's unless x' lies within D
 // of an integer.  Those values (about 1 in 10^4, zero included) and operands outside
 // the reciprocal's comfortable range take the exact path: IEEE division, double product.
+// BOUNDED: the samples are integers of a recorded format (|x| <= 2^15), so ab1 < 2^55 and
+// the reciprocal never leaves the normal range on the large side; ab1 = 0 (or a denormal
+// the reciprocal flushes) makes x' inf or NaN, so e is NaN and !(e >= D) takes the exact
+// path -- the range compare is only needed for cf32 input of arbitrary magnitude
+template <bool BOUNDED = false>
 __device__ __forceinline__ bool soft_fast(float2 r1, float ab1, int &ir, int &ii) {
 #pragma clang fp contract(off)
     constexpr float D = 0x1p-14f;
     const float m = __builtin_amdgcn_rcpf(ab1) * -127.0f;
     const float xr = r1.x * m, xi = r1.y * m;
     const float e = fminf(fabsf(xr - rintf(xr)), fabsf(xi - rintf(xi)));
-    // ab1 (>= 0 or NaN) outside [2^-100, 2^100]: one unsigned compare on its bits
-    const bool range = (__float_as_uint(ab1) - 0x0D800000u) > 0x64000000u;
     ir = (int)xr;
     ii = (int)xi;
-    return e < D || range;
+    if constexpr (BOUNDED) {
+        return !(e >= D);
+    } else {
+        // ab1 (>= 0 or NaN) outside [2^-100, 2^100]: one unsigned compare on its bits
+        const bool range = (__float_as_uint(ab1) - 0x0D800000u) > 0x64000000u;
+        return e < D || range;
+    }
 }
 __device__ __forceinline__ void soft_pair(float2 r1, float ab1, int &ir, int &ii) {
     if (soft_fast(r1, ab1, ir, ii)) {
@@ -452,30 +461,30 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
         // off: byte offset from block 0; the prefetch registers hold the raw samples (8, 4
         // or 2 bytes), converted when the symbol's turn comes
         auto ld = [&](int32_t off) -> typename Fmt::raw { return Fmt::load(rin, off); };
-        float2 a[8], P[8];
+        // the spectra of symbols l and l - 1 alternate between A and B (the loop runs two
+        // symbols per trip), so neither is copied into the other per symbol
+        float2 A[8], B[8];
         typename Fmt::raw nx[8], ng6, ng7;
         // warm-up symbol l0 - 1 (block 0, the PRS, for the first chunk)
         {
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
             const int32_t o = ((l0 - 1) * TS + t) * BPS;
 #pragma unroll
-            for (int m = 0; m < 8; m++) a[m] = Fmt::scaled(ld(o + 256 * BPS * m));
-            if (l0 == 1) mix<GEN>(a, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
-            else mix<GEN>(a, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
+            for (int m = 0; m < 8; m++) B[m] = Fmt::scaled(ld(o + 256 * BPS * m));
+            if (l0 == 1) mix<GEN>(B, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
+            else mix<GEN>(B, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
         }
         int32_t ov = (l0 * TS + t) * BPS;                     // this thread's sample 0 of symbol l
         ng6 = ld(ov - 512 * BPS);
         ng7 = ld(ov - 256 * BPS);
 #pragma unroll
         for (int m = 0; m < 8; m++) nx[m] = ld(ov + 256 * BPS * m);
-        fft2048_wg(a, ex, tw, t);
+        fft2048_wg(B, ex, tw, t);
         if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
-            const int16_t v = snr_wg(a, t, red, Fmt::unscale);
+            const int16_t v = snr_wg(B, t, red, Fmt::unscale);
             if (t == 0) aux.snr[fi] = v;
         }
         __syncthreads();                                // pass 3 read ex: the first symbol's pass 1 writes it
-#pragma unroll
-        for (int k = 0; k < 8; k++) P[k] = a[k];
         // NCO of segment B (round 4): thread t's samples of symbol l are n = t + 256 m, so
         // their oscillatorTable indices step by -d256 per m and by -dsym per symbol (mod
         // 2048000).  The exact e^{2 pi i ti / N} of the chunk's first sample (the factor
@@ -510,13 +519,16 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
 
             efc = nco_value(ncl, nco_mod(-(int64_t)TU * ph));
         }
-        for (int l = l0; l < l1; l++) {
+        // symbol l: a = its spectrum (computed here), P = symbol l - 1's
+        auto sym = [&](const int l, float2 (&a)[8], const float2 (&P)[8]) __attribute__((always_inline)) {
             // this symbol's samples and its guard samples, all loaded one symbol ahead
-            // (a guard load issued here would expose a full HBM latency per symbol)
+            // (a guard load issued here would expose a full HBM latency per symbol).  The
+            // loads after the chunk's last symbol are not conditional: past the frame they
+            // read the buffer's out-of-range zeros, inside it a symbol nobody uses
 #pragma unroll
             for (int m = 0; m < 8; m++) a[m] = Fmt::scaled(nx[m]);
             const float2 g6 = Fmt::scaled(ng6), g7 = Fmt::scaled(ng7);
-            if (l + 1 < l1) {
+            {
                 const int32_t o1 = ov + TS * BPS;
                 ng6 = ld(o1 - 512 * BPS);
                 ng7 = ld(o1 - 256 * BPS);
@@ -577,7 +589,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
                 // ab1 = |re| + |im| (ofdm-decoder.cpp:185-189)
                 const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                 int ir, ii;
-                risky |= soft_fast(r1, ab1, ir, ii);
+                risky |= soft_fast<FMT != DABGPU_IQ_F32>(r1, ab1, ir, ii);
                 const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
                 *(uint32_t *)((char *)st + addr) = spair(ir, ii);
             }
@@ -587,7 +599,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
                     const float2 r1 = cmul_conj_exact(a[k], P[k]);
                     const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                     int ir, ii;
-                    if (soft_fast(r1, ab1, ir, ii)) {
+                    if (soft_fast<FMT != DABGPU_IQ_F32>(r1, ab1, ir, ii)) {
                         const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
                         *(uint32_t *)((char *)st + addr) = spair(trunc127d(-r1.x / ab1), trunc127d(-r1.y / ab1));
                     }
@@ -607,8 +619,6 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
                     }
                 }
             }
-#pragma unroll
-            for (int k = 0; k < 8; k++) P[k] = a[k];
             __syncthreads();
             // carriers 4q..4q+3, q < 384: re to row[4q..], im to row[K + 4q..]
             const int32_t rowb = (l - 1) * SYMBITS * esz;
@@ -644,6 +654,10 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
                 }
             }
             __syncthreads();
+        };
+        for (int l = l0; l < l1; l += 2) {
+            sym(l, A, B);
+            if (l + 1 < l1) sym(l + 1, B, A);
         }
         fc = cmulw(fc, efc);
         fc.x *= Fmt::unscale * Fmt::unscale;           // the partial sums in absolute units (exact)

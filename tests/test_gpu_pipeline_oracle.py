@@ -185,6 +185,32 @@ def test_pipeline_dropout_reacquires_like_reference(ctx, fmt):
 
 
 @FMTS
+def test_pipeline_digital_silence_like_reference(ctx, fmt):
+    """exact zero samples over six data symbols of a frame (a recording's digital
+    silence): their spectra are 0, so r = X conj(P) = 0 and q = -re / (|re| + |im|) is
+    0 / 0 in the reference (ofdm-decoder.cpp:185-189) -- the soft-bit fast path must hand
+    those bins to the exact path (NaN -> the same int16 as the reference's conversion) on
+    both formats (the bounded formats decide it without the range compare), and the frame
+    after them decodes as the reference's"""
+    from dabamd.synth import Ensemble
+    sub = MIXED[:3]
+    F, runs = 4, 2
+    e = Ensemble(F * runs + 4, subch=sub, snr_db=25.0, amplitude=_amp(fmt))
+    g = e.generate(53, truth=False)
+    iq = g["iq"].reshape(-1, 2).copy()
+    a = g["frame0"] + 2 * 196608 + 20000           # data symbols ~7..13 of the third frame
+    iq[a:a + 6 * 2552] = 0.0
+    iq = pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt)
+    ref = orc.decode_stream(iq, F * runs, sub)
+    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt)
+    st = pc.compare(gpu[0], ref, sub)
+    print("silence:", st)
+    _check([st], "silence")
+    assert st["frames"] == ref["n"] >= F * runs - 1
+    ctx.check()
+
+
+@FMTS
 def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
     """DABGPU_CTL_ACQ_ASYNC: stream 0 loses sync in a dropout (as above); its null search
     runs in the background while stream 1 keeps decoding n_frames per run, and the runs
