@@ -346,6 +346,25 @@ class Context:
             stage.free()
         return dst, n
 
+    def load_recording(self, path: str, max_pairs: Optional[int] = None, chunk_pairs: int = 1 << 25):
+        """Read a .raw (u8) or .sdr (WAV PCM16) recording into HBM as the file holds it
+        (2 or 4 bytes per I/Q pair, a quarter / half of cf32): the pipeline converts it in
+        its kernels' loads (Pipeline.set_iq_format(fmt), exactly as the reference's readers
+        do, rawfiles.cpp:115-117 / wavfiles.cpp:172).  Streamed in chunks from the
+        memory-mapped file.  Returns (DevBuf, n_pairs, fmt)."""
+        if path.endswith(".raw"):
+            src, fmt, w = read_raw(path), IQ_U8, 1
+        else:
+            src, fmt, w = read_sdr(path), IQ_S16, 2
+        n = src.size // 2
+        if max_pairs is not None:
+            n = min(n, int(max_pairs))
+        dst = self.buf(max(2 * w * n, 16))
+        for p0 in range(0, n, chunk_pairs):
+            m = min(chunk_pairs, n - p0)
+            dst.upload_at(np.ascontiguousarray(src[2 * p0: 2 * (p0 + m)]), 2 * w * p0)
+        return dst, n, fmt
+
     def check(self) -> None:
         """raise if a kernel refused out-of-bounds work since the last check"""
         _chk(lib().dabgpu_kernel_errors(self.h), "kernel bounds check")

@@ -40,23 +40,28 @@ def to_raw(iq, fmt):
 
 
 def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=(), dabplus=False, packed=False,
-               acq_async=False, packed_pad=0, iq_format=IQ_F32):
+               acq_async=False, packed_pad=0, iq_format=IQ_F32, dev_iq=None):
     """Decode `runs` x F frames of every stream.  iqs: list of float32 IQ arrays
     (interleaved); n_avail: optional list (per run) of per-stream available sample
     counts.  iq_format: the streams go to the GPU as that recorded format (iqs must be
     representable: quantize()), read by the kernels through dabgpu_pipe_set_iq_format.
+    dev_iq: (DevBuf, stride) already in HBM in that format (e.g. Context.load_recording)
+    instead of uploading iqs (which then only give the stream lengths).
     Returns per stream: dict(info [frames], fic, crc, msc {cif: [nsub][nb]},
     soft {frame: [75][3072]} for soft_streams, sf {cif: [(info, bytes)...]})."""
     import dabamd
     S = len(iqs)
     lens = [len(x) // 2 for x in iqs]
     stride = max(lens)
-    dt = {IQ_F32: np.float32, IQ_S16: np.int16, IQ_U8: np.uint8}[iq_format]
-    buf = np.zeros((S, 2 * stride), dt)
-    for s, x in enumerate(iqs):
-        buf[s, :len(x)] = to_raw(x, iq_format)
-    diq = ctx.put(buf)
-    del buf
+    if dev_iq is not None:
+        diq, stride = dev_iq
+    else:
+        dt = {IQ_F32: np.float32, IQ_S16: np.int16, IQ_U8: np.uint8}[iq_format]
+        buf = np.zeros((S, 2 * stride), dt)
+        for s, x in enumerate(iqs):
+            buf[s, :len(x)] = to_raw(x, iq_format)
+        diq = ctx.put(buf)
+        del buf
     subs = [dabamd.Subch(sc[0], sc[1], sc[2], sc[3], 0 if sc[4] else 1,
                          dabamd.SUBCH_DABPLUS if (len(sc) > 5 and sc[5]) else 0) for sc in subch]
     dpi = [k for k, sc in enumerate(subch) if len(sc) > 5 and sc[5]]
@@ -109,7 +114,8 @@ def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=()
                 nfr[s] += nf
     finally:
         pipe.close()
-        diq.free()
+        if dev_iq is None:
+            diq.free()
     for s in range(S):
         out[s]["fic"] = np.array(out[s]["fic"]).reshape(-1, 4, 768)
         out[s]["crc"] = np.array(out[s]["crc"]).reshape(-1, 12)

@@ -423,6 +423,37 @@ def test_recorded_format_decodes_like_converted_cf32(ctx, fmt):
         assert all(np.array_equal(a[s]["soft"][g], b[s]["soft"][g]) for g in a[s]["soft"])
 
 
+@pytest.mark.parametrize("fmt", [S16, U8], ids=["sdr", "raw"])
+def test_recording_file_decodes_from_hbm_like_reference(ctx, fmt, tmp_path):
+    """a recording file (.sdr WAV PCM16, gui.cpp:880-883, or .raw u8) read into HBM as
+    the file holds it (Context.load_recording: 4 / 2 bytes per pair, memory-mapped and
+    streamed) and decoded by the pipeline straight from those bytes: the bytes equal the
+    file's, and placement, soft bits, FIC and MSC equal the oracle's decode of the samples
+    the reference's reader would hand over"""
+    import dabamd
+    sub = MIXED[:2]
+    F, runs = 4, 2
+    iq = _gen(sub, F * runs + 1, [81], 15.0, 600.0, fmt)[0]
+    raw = pc.to_raw(iq, fmt)
+    path = tmp_path / ("rec.sdr" if fmt == S16 else "rec.raw")
+    if fmt == S16:
+        dabamd.write_sdr(str(path), raw)
+    else:
+        raw.tofile(str(path))
+    buf, n, got_fmt = ctx.load_recording(str(path), chunk_pairs=1 << 20)
+    try:
+        assert got_fmt == fmt and n == len(iq) // 2
+        assert np.array_equal(buf.download(raw.dtype, raw.shape), raw)
+        ref = orc.decode_stream(iq, F * runs, sub)
+        gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt, dev_iq=(buf, n))
+        st = pc.compare(gpu[0], ref, sub)
+        print("recording:", fmt, st)
+        _check([st], "recording")
+        assert st["frames"] == ref["n"] >= F * runs - 1
+    finally:
+        buf.free()
+
+
 def _profile_mix():
     """subchannels covering the depuncturing kinds the pipeline's input-major ACS loader
     meets (k_viterbi.hip acs_tiles_in): UEP rows with rate-1/4 segments (PI 24: 240
