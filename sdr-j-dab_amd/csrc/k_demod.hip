@@ -105,6 +105,25 @@ __device__ __forceinline__ float quad_bfly(float v, float sign) {
     return fmaf(sign, v, p);
 }
 
+// the same butterfly with the lane's sign on the partner: own + sign * partner (upper lanes
+// get minus the butterfly's value; fft2048_wg<true> tracks that sign as tw.tau)
+// The compiler does not fold a DPP move into v_fmac_f32 (it folds add / mul), so the fused
+// form is written out: v_fmac_f32_dpp acc = dpp(src) * sign + acc with acc = src = v, one
+// VALU instead of a DPP move and an fma, the same single rounding.  The s_nop 1 is the two
+// wait states a DPP read needs after the VALU write of its source (the hazard recognizer
+// does not look inside inline assembly).
+template <int M>
+__device__ __forceinline__ float quad_bfly_s(float v, float sign) {
+    float r;
+    if constexpr (M == 2)
+        asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                     : "=v"(r) : "v"(v), "v"(sign), "0"(v));
+    else
+        asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+                     : "=v"(r) : "v"(v), "v"(sign), "0"(v));
+    return r;
+}
+
 // v[m] *= oscillatorTable[localPhase] sample by sample (ofdm-processor.cpp:186-201).
 // GEN: localPhase steps by -phase per sample, the table rebuilt from the factor tables
 // in LDS (nco_value; the 16 MB table itself would cost a cache line per sample);
@@ -146,10 +165,18 @@ struct DemodTw {
     const float2 *w2;             // LDS table W256^(t' k) at [(k - 1) * 32 + t']: consecutive lanes, no bank conflicts
     const float2 *w3;             // LDS table W32^(t'' k) at [(k - 1) * 4 + t'']: a quad's 4 values in 4 different banks
     float sg2, sg1;               // quad butterfly signs (+1 lower lane, -1 upper)
+    float tau;                    // fft2048_wg<true>'s output sign of this lane (t'' = 1, 2: -1)
     bool rot;                     // lane t'' == 3 multiplies by -j between the two stages
 };
 
-// the FFT of the 8 samples a[] (n = t + 256 m) of every thread; ex: 2048 + pad float2 of LDS
+// the FFT of the 8 samples a[] (n = t + 256 m) of every thread; ex: 2048 + pad float2 of LDS.
+// SIGNED: each lane's outputs come out times tw.tau (+-1, exact): pass 4's butterflies then
+// take the partner's value as the fma's multiplicand (own + sign * partner), which the
+// compiler folds into one v_fmac_f32_dpp per value and stage instead of a DPP move and an
+// fma.  For DQPSK the sign cancels (X_l conj(X_{l-1}) with both scaled by the same tau: the
+// same products, bit for bit), and |X| is unchanged; the callers that need X itself use
+// SIGNED = false.
+template <bool SIGNED = false>
 __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const DemodTw &tw, int t) {
     // pass 1
     dft8(a);
@@ -181,9 +208,15 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
     // pass 4: radix-4 over the quad's t''; lane t'' ends with K'' = brev2(t'')
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        float2 v = make_float2(quad_bfly<2>(a[k].x, tw.sg2), quad_bfly<2>(a[k].y, tw.sg2));
-        if (tw.rot) v = make_float2(v.y, -v.x);
-        a[k] = make_float2(quad_bfly<1>(v.x, tw.sg1), quad_bfly<1>(v.y, tw.sg1));
+        if constexpr (SIGNED) {
+            float2 v = make_float2(quad_bfly_s<2>(a[k].x, tw.sg2), quad_bfly_s<2>(a[k].y, tw.sg2));
+            if (tw.rot) v = make_float2(v.y, -v.x);
+            a[k] = make_float2(quad_bfly_s<1>(v.x, tw.sg1), quad_bfly_s<1>(v.y, tw.sg1));
+        } else {
+            float2 v = make_float2(quad_bfly<2>(a[k].x, tw.sg2), quad_bfly<2>(a[k].y, tw.sg2));
+            if (tw.rot) v = make_float2(v.y, -v.x);
+            a[k] = make_float2(quad_bfly<1>(v.x, tw.sg1), quad_bfly<1>(v.y, tw.sg1));
+        }
     }
 }
 
@@ -208,6 +241,7 @@ __device__ __forceinline__ DemodTw tw_setup(TwLds &L, const OfdmTables &T, int t
     tw.w3 = L.w3;
     tw.sg2 = (tq & 2) ? -1.0f : 1.0f;
     tw.sg1 = (tq & 1) ? -1.0f : 1.0f;
+    tw.tau = (tq == 1 || tq == 2) ? -1.0f : 1.0f;
     tw.rot = tq == 3;
     return tw;
 }
@@ -479,7 +513,7 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
         ng7 = ld(ov - 256 * BPS);
 #pragma unroll
         for (int m = 0; m < 8; m++) nx[m] = ld(ov + 256 * BPS * m);
-        fft2048_wg(B, ex, tw, t);
+        fft2048_wg<true>(B, ex, tw, t);
         if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
             const int16_t v = snr_wg(B, t, red, Fmt::unscale);
             if (t == 0) aux.snr[fi] = v;
@@ -564,14 +598,15 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
 #pragma unroll
                 for (int m = 0; m < 8; m++) mp[t + 256 * m] = a[m];
             }
-            fft2048_wg(a, ex, tw, t);
+            fft2048_wg<true>(a, ex, tw, t);
             if (aux.disp && l == aux.disp_token) {     // the display token's carriers (ofdm-decoder.cpp:197-205)
                 float2 *dp = aux.disp + (int64_t)fr.out_slot * K;
                 const int b0 = bin0_of(t);
 #pragma unroll
                 for (int k = 0; k < 8; k++) {
                     const int b = b0 + 64 * k;
-                    const float2 v = make_float2(a[k].x * Fmt::unscale, a[k].y * Fmt::unscale);
+                    const float s = tw.tau * Fmt::unscale;     // a power of two, signed: exact
+                    const float2 v = make_float2(a[k].x * s, a[k].y * s);
                     if (b < K / 2) dp[b] = v;
                     else if (b >= TU - 1 - K / 2 && b < TU - 1) dp[b - (TU - 1 - K)] = v;
                 }
