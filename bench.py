@@ -700,10 +700,10 @@ def main():
                         "span on its stream: the demod is queued once run r-2's ACS is done, so its span includes "
                         "the time its workgroups wait for the slots the running ACS still holds; frac_alone is the "
                         "kernel's own rate.  The demod is not HBM-bound: halving its input bytes (PCM16) left its "
-                        "time alone unchanged (profiles/r05_iq_format_ab.txt); it answers to VALU count (~1,000 "
-                        "VALU per wave-symbol, the SIMDs' VALU busy ~75 % of the time at the measured per-opcode "
-                        "rates; 80 fewer VALU per symbol made it 10 % faster alone, "
-                        "profiles/r05_demod_micro_ab.txt, DESIGN section 9)"}
+                        "time alone unchanged (profiles/r05_iq_format_ab.txt); it answers partly to VALU count (its "
+                        "SIMDs' VALU busy ~70 % of the time at the measured per-opcode rates; round 5's instruction "
+                        "cuts, -16 % SQ_INSTS_VALU in the same dispatch, made it 8 % faster: "
+                        "profiles/r05e_pmc_issue_c3.txt vs r05w_pmc_issue_c3.txt, DESIGN section 9)"}
     roof_hbm["frac"] = roof_hbm["achieved"] / roof_hbm["peak"]
     if tm_alone.get("demod"):
         roof_hbm["ms_per_launch"] = demod_ms
