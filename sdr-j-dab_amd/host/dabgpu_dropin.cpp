@@ -3,6 +3,8 @@
 // (or a few) kernel launches and one download on the thread's HIP stream.
 #include "dabgpu_dropin.h"
 
+#include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -282,6 +284,109 @@ void ensembleDecoder::load(const std::vector<const DSPCOMPLEX *> &samples, const
             "dabgpu_memcpy_h2d");
     navail_ = n;
     frames_done_.assign(cfg_.n_streams, 0);
+    chk(dabgpu_pipe_set_iq_format(pipe_, DABGPU_IQ_F32), "dabgpu_pipe_set_iq_format");
+}
+
+void ensembleDecoder::load_recorded(int format, const std::vector<const void *> &samples, const std::vector<int64_t> &n) {
+    if ((int)samples.size() != cfg_.n_streams || (int)n.size() != cfg_.n_streams)
+        throw error(DABGPU_E_ARG, "ensembleDecoder::load_recorded: one sample array per stream");
+    if (format != DABGPU_IQ_S16 && format != DABGPU_IQ_U8)
+        throw error(DABGPU_E_ARG, "ensembleDecoder::load_recorded: format DABGPU_IQ_S16 or DABGPU_IQ_U8");
+    const size_t bps = format == DABGPU_IQ_S16 ? 4 : 2;      // bytes per I/Q pair
+    stride_ = 0;
+    for (int64_t k : n) stride_ = std::max(stride_, k);
+    iq_.resize(bps * (size_t)stride_ * cfg_.n_streams);
+    for (int s = 0; s < cfg_.n_streams; s++)
+        chk(dabgpu_memcpy_h2d(thread_context(), (char *)iq_.get() + bps * stride_ * s, samples[s], bps * n[s]),
+            "dabgpu_memcpy_h2d");
+    navail_ = n;
+    frames_done_.assign(cfg_.n_streams, 0);
+    chk(dabgpu_pipe_set_iq_format(pipe_, format), "dabgpu_pipe_set_iq_format");
+}
+
+namespace {
+// the data chunk of an .sdr recording: what wavFiles accepts (wavfiles.cpp:56-69 via
+// libsndfile: 2 channels, 2048000 Hz, 16-bit PCM; WAVE_FORMAT_EXTENSIBLE with the PCM
+// subformat too).  Returns the payload's byte offset and size.
+std::pair<int64_t, int64_t> sdr_payload(std::FILE *f, const std::string &path) {
+    auto u32 = [](const uint8_t *b) { return (uint32_t)b[0] | (uint32_t)b[1] << 8 | (uint32_t)b[2] << 16 | (uint32_t)b[3] << 24; };
+    auto u16 = [](const uint8_t *b) { return (uint32_t)b[0] | (uint32_t)b[1] << 8; };
+    uint8_t h[12];
+    if (std::fread(h, 1, 12, f) != 12 || std::memcmp(h, "RIFF", 4) || std::memcmp(h + 8, "WAVE", 4))
+        throw error(DABGPU_E_ARG, path + ": not a RIFF/WAVE file");
+    int64_t off = 12;
+    bool fmt_ok = false, have_fmt = false;
+    for (;;) {
+        uint8_t ck[8];
+        if (std::fread(ck, 1, 8, f) != 8) throw error(DABGPU_E_ARG, path + ": no data chunk");
+        const int64_t n = u32(ck + 4);
+        off += 8;
+        if (!std::memcmp(ck, "fmt ", 4)) {
+            std::vector<uint8_t> b((size_t)n);
+            if (n < 16 || std::fread(b.data(), 1, (size_t)n, f) != (size_t)n) throw error(DABGPU_E_ARG, path + ": bad fmt chunk");
+            uint32_t tag = u16(&b[0]);
+            if (tag == 0xFFFE && n >= 26) tag = u16(&b[24]);       // WAVE_FORMAT_EXTENSIBLE: the subformat
+            fmt_ok = tag == 1 && u16(&b[2]) == 2 && u32(&b[4]) == 2048000 && u16(&b[14]) == 16;
+            have_fmt = true;
+            if (n & 1) std::fseek(f, 1, SEEK_CUR);
+        } else if (!std::memcmp(ck, "data", 4)) {
+            if (!have_fmt || !fmt_ok)
+                throw error(DABGPU_E_ARG, path + ": not a recorded DAB file (need PCM16, 2 channels, 2048000 Hz)");
+            return {off, n};
+        } else {
+            std::fseek(f, (long)(n + (n & 1)), SEEK_CUR);
+        }
+        off += n + (n & 1);
+    }
+}
+}  // namespace
+
+void ensembleDecoder::load_files(const std::vector<std::string> &paths) {
+    if ((int)paths.size() != cfg_.n_streams) throw error(DABGPU_E_ARG, "ensembleDecoder::load_files: one file per stream");
+    auto is_raw = [](const std::string &p) { return p.size() >= 4 && p.compare(p.size() - 4, 4, ".raw") == 0; };
+    const bool raw = !paths.empty() && is_raw(paths[0]);
+    for (const std::string &p : paths)
+        if (is_raw(p) != raw) throw error(DABGPU_E_ARG, "ensembleDecoder::load_files: .raw and .sdr files mixed");
+    const int format = raw ? DABGPU_IQ_U8 : DABGPU_IQ_S16;
+    const size_t bps = raw ? 2 : 4;
+    struct closer { void operator()(std::FILE *f) const { if (f) std::fclose(f); } };
+    std::vector<std::unique_ptr<std::FILE, closer>> files;
+    std::vector<std::pair<int64_t, int64_t>> payload;
+    std::vector<int64_t> n;
+    for (const std::string &p : paths) {
+        std::unique_ptr<std::FILE, closer> f(std::fopen(p.c_str(), "rb"));
+        if (!f) throw error(DABGPU_E_ARG, p + ": cannot open");
+        std::pair<int64_t, int64_t> pl{0, 0};
+        if (raw) {
+            std::fseek(f.get(), 0, SEEK_END);
+            pl = {0, (int64_t)std::ftell(f.get())};
+        } else {
+            pl = sdr_payload(f.get(), p);
+            std::fseek(f.get(), 0, SEEK_END);
+            pl.second = std::min<int64_t>(pl.second, (int64_t)std::ftell(f.get()) - pl.first);   // a truncated recording
+        }
+        n.push_back(pl.second / (int64_t)bps);
+        payload.push_back(pl);
+        files.push_back(std::move(f));
+    }
+    stride_ = 0;
+    for (int64_t k : n) stride_ = std::max(stride_, k);
+    iq_.resize(bps * (size_t)stride_ * cfg_.n_streams);
+    std::vector<char> piece((size_t)1 << 24);
+    for (int s = 0; s < cfg_.n_streams; s++) {
+        std::FILE *f = files[s].get();
+        std::fseek(f, (long)payload[s].first, SEEK_SET);
+        for (int64_t done = 0, total = n[s] * (int64_t)bps; done < total;) {
+            const size_t want = (size_t)std::min<int64_t>((int64_t)piece.size(), total - done);
+            if (std::fread(piece.data(), 1, want, f) != want) throw error(DABGPU_E_ARG, paths[s] + ": short read");
+            chk(dabgpu_memcpy_h2d(thread_context(), (char *)iq_.get() + bps * stride_ * s + done, piece.data(), want),
+                "dabgpu_memcpy_h2d");
+            done += (int64_t)want;
+        }
+    }
+    navail_ = n;
+    frames_done_.assign(cfg_.n_streams, 0);
+    chk(dabgpu_pipe_set_iq_format(pipe_, format), "dabgpu_pipe_set_iq_format");
 }
 
 void ensembleDecoder::acquire() {

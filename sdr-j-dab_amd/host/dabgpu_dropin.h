@@ -462,6 +462,14 @@ public:
     void on_superframe(sf_cb f) { sf_cb_ = std::move(f); }
     // samples[s] -> n[s] cf32 samples of stream s (copied to HBM)
     void load(const std::vector<const DSPCOMPLEX *> &samples, const std::vector<int64_t> &n);
+    // the streams as recorded: format DABGPU_IQ_S16 (.sdr PCM16 I/Q pairs) or DABGPU_IQ_U8
+    // (.raw bytes), n[s] pairs each, copied to HBM as they are -- the pipeline converts them
+    // in its sample loads with the readers' scaling (wavfiles.cpp:172, rawfiles.cpp:115-117)
+    void load_recorded(int format, const std::vector<const void *> &samples, const std::vector<int64_t> &n);
+    // one recording file per stream, all .sdr (RIFF/WAVE PCM16, 2 channels, 2048000 Hz, as
+    // wavFiles accepts them: wavfiles.cpp:56-69) or all .raw (u8 I/Q): read in pieces straight
+    // into HBM, unconverted.  Throws dabgpu::error for any other file.
+    void load_files(const std::vector<std::string> &paths);
     // null search (ofdm-processor.cpp:274-338) for every unsynchronised stream from its
     // current position (optional: step() acquires such streams itself)
     void acquire();

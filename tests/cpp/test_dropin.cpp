@@ -7,6 +7,7 @@
 #include <cstdio>
 #include <mutex>
 #include <thread>
+#include <unistd.h>
 #include <cstdlib>
 #include <cstring>
 #include <random>
@@ -197,6 +198,82 @@ int main() {
         CHECK(msc_n == 2 * (NC - 16) * 3 && msc_bad == 0, "MSC %d bad %d", msc_n, msc_bad);
         CHECK(sf_ok >= 2 * 2 * 3 && sf_bad == 0, "superframes ok %d bad %d", sf_ok, sf_bad);
         std::printf("ensembleDecoder: ok (%d FIBs, %d MSC CIF-subchannels, %d superframes)\n", fib_n, msc_n, sf_ok);
+    }
+    // ensembleDecoder::load_files: an ensemble recorded as an .sdr file (RIFF/WAVE PCM16,
+    // written through the drop-in's libsndfile subset, gui.cpp:880-883) and as a .raw file
+    // (u8 I/Q), decoded from HBM as the files hold them: every FIB CRC-good, every MSC
+    // CIF-subchannel equal to the transmitted bits
+    {
+        dabsynth_subch sc[2] = {{0, 96, 128, 3, 1, 0}, {96, 48, 64, 0103, 0, 1}};
+        dabsynth_cfg cfg;
+        std::memset(&cfg, 0, sizeof cfg);
+        const int F = 3, runs = 2;
+        cfg.n_frames = F * runs;
+        cfg.pre_offset = 50000;
+        cfg.snr_db = 30.0f;
+        cfg.amplitude = 0.25f;                           // a recording's gain: peaks inside +-1
+        cfg.n_subch = 2;
+        cfg.subch = sc;
+        const int64_t n = dabsynth_stream_len(&cfg);
+        const int NC = 4 * F * runs, maxbits = 24 * 128;
+        std::vector<float> iq(2 * n);
+        std::vector<uint8_t> msc((size_t)NC * 2 * maxbits);
+        int64_t f0;
+        dabsynth_generate(&cfg, 321, iq.data(), nullptr, msc.data(), nullptr, &f0);
+        for (int raw = 0; raw < 2; raw++) {
+            char path[64];
+            std::snprintf(path, sizeof path, "/tmp/dabgpu_rec_%d.%s", (int)getpid(), raw ? "raw" : "sdr");
+            if (raw) {
+                std::vector<uint8_t> b(2 * n);
+                for (int64_t i = 0; i < 2 * n; i++)
+                    b[i] = (uint8_t)std::min(255.0f, std::max(0.0f, std::nearbyint(iq[i] * 128.0f + 128.0f)));
+                std::FILE *f = std::fopen(path, "wb");
+                CHECK(f && std::fwrite(b.data(), 1, b.size(), f) == b.size(), "write %s", path);
+                if (f) std::fclose(f);
+            } else {
+                std::vector<int16_t> b(2 * n);
+                for (int64_t i = 0; i < 2 * n; i++)
+                    b[i] = (int16_t)std::min(32767.0f, std::max(-32768.0f, std::nearbyint(iq[i] * 32768.0f)));
+                dabgpu::SF_INFO info{0, 2048000, 2, dabgpu::SF_FORMAT_WAV | dabgpu::SF_FORMAT_PCM_16, 0, 0};
+                dabgpu::SNDFILE *f = dabgpu::sf_open(path, dabgpu::SFM_WRITE, &info);
+                CHECK(f && dabgpu::sf_writef_short(f, b.data(), n) == n, "write %s", path);
+                if (f) dabgpu::sf_close(f);
+            }
+            dabgpu::ensembleDecoder::config ec;
+            ec.n_streams = 1;
+            ec.n_frames = F;
+            ec.subch = {{0, 96, 128, 3, 0, 0}, {96, 48, 64, 0103, 1, DABGPU_SUBCH_DABPLUS}};
+            dabgpu::ensembleDecoder dec(ec);
+            int fib_n = 0, fib_bad = 0, msc_n = 0, msc_bad = 0;
+            dec.on_fib([&](int, int64_t, int, const uint8_t *, bool ok) { fib_n++; fib_bad += !ok; });
+            dec.on_msc([&](int, int64_t cif, int k, const uint8_t *bits, int nbits) {
+                msc_n++;
+                if (std::memcmp(bits, msc.data() + ((size_t)cif * 2 + k) * maxbits, nbits)) msc_bad++;
+            });
+            dec.load_files({path});
+            dec.acquire();
+            for (int r = 0; r < runs; r++) CHECK(dec.step(), "%s step %d", path, r);
+            std::remove(path);
+            CHECK(fib_n == F * runs * 12 && fib_bad == 0, "%s: FIBs %d bad %d", path, fib_n, fib_bad);
+            CHECK(msc_n == (NC - 16) * 2 && msc_bad == 0, "%s: MSC %d bad %d", path, msc_n, msc_bad);
+            std::printf("ensembleDecoder::load_files (%s): ok (%d FIBs, %d MSC CIF-subchannels)\n",
+                        raw ? ".raw u8" : ".sdr PCM16", fib_n, msc_n);
+        }
+        bool threw = false;                              // any other WAV layout is refused
+        try {
+            const char *bad = "/tmp/dabgpu_bad.sdr";
+            std::FILE *f = std::fopen(bad, "wb");
+            if (f) { std::fwrite("RIFF\0\0\0\0WAVEjunk", 1, 16, f); std::fclose(f); }
+            dabgpu::ensembleDecoder::config ec;
+            ec.n_streams = 1;
+            ec.n_frames = F;
+            dabgpu::ensembleDecoder dec(ec);
+            dec.load_files({bad});
+        } catch (const dabgpu::error &) {
+            threw = true;
+        }
+        std::remove("/tmp/dabgpu_bad.sdr");
+        CHECK(threw, "a malformed .sdr file is refused");
     }
     // a functional ficHandler: the GPU-decoded FIBs of an ensemble that describes
     // itself (FIG 0/1, 0/2, 1/0, 1/1) configure the MSC decoder through
