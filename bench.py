@@ -84,7 +84,9 @@ def dist_setup(n_gpus):
     if world != n_gpus:
         raise SystemExit(f"bench.py: --gpus {n_gpus} but WORLD_SIZE={world}")
     dist = None
-    if world > 1:
+    # DAB_DIST_FORCE=1: a one-rank process group too (RCCL on a GPU box) -- a rehearsal of the
+    # N > 1 code paths (collectives, the C4 leg's transport) on one GPU
+    if world > 1 or os.environ.get("DAB_DIST_FORCE") == "1":
         import torch
         import torch.distributed as td
         ngpu = torch.cuda.device_count()
@@ -94,7 +96,16 @@ def dist_setup(n_gpus):
             torch.cuda.set_device(local)
         td.init_process_group(backend=backend)
         dist = td
+        # the ranks' barriers, time reductions and check gathers go through a gloo group on
+        # the host: an RCCL communicator, once created, slows this process's pipeline by ~9 %
+        # (profiles/r05_rccl_overhead_ab.txt), so RCCL is used only where the data moves (the C4
+        # leg's transfers, after the rank-local legs)
+        global _CTL
+        _CTL = td.new_group(backend="gloo") if backend == "nccl" else None
     return rank, local, world, dist
+
+
+_CTL = None     # the control group (gloo) beside an RCCL default group
 
 
 def rank_device(local):
@@ -114,16 +125,15 @@ def rank_seed0(rank, ensembles):
 
 def barrier(dist):
     if dist is not None:
-        dist.barrier()
+        dist.barrier(group=_CTL)
 
 
 def allreduce_max(dist, x):
     if dist is None:
         return x
     import torch
-    dev = "cuda" if torch.cuda.is_available() and dist.get_backend() == "nccl" else "cpu"
-    t = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    t = torch.tensor([x], dtype=torch.float64)       # on the host: the gloo control group
+    dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_CTL)
     return float(t.item())
 
 
@@ -289,7 +299,7 @@ def gather_objects(dist, obj):
     if dist is None:
         return [obj]
     out = [None] * dist.get_world_size()
-    dist.all_gather_object(out, obj)
+    dist.all_gather_object(out, obj, group=_CTL)
     return out
 
 
@@ -519,7 +529,7 @@ def main():
         sys.exit(launch_ranks(args.gpus))
     rank, local, world, dist = dist_setup(args.gpus)
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and dist is None and not args.no_cpu_baseline:
         # before this process touches the GPU: the workers are forked children
         cpu = cpu_baseline(budget_s=args.cpu_seconds, workload=args.workload, cfo=args.cfo)
     import dabamd
@@ -539,7 +549,7 @@ def main():
     ctx = dabamd.Context(rank_device(local))
     stride = ens.length
     threads = min(16, os.cpu_count() or 1)
-    fed = world > 1 and not args.no_c4_fed
+    fed = (world > 1 or dist is not None) and not args.no_c4_fed
     cs, _ = chunk_layout(stride, F)
     fed_ph = np.zeros((P * TF // cs, E, 2 * cs), FORMATS[args.fed_format][2]) if fed else None
     # Every stream is cyclic (dabsynth_generate_period: P frames repeated end to end, a
