@@ -209,12 +209,15 @@ def p2p_batch(dist, sends, recvs):
     import torch
     import torch.distributed as td
     staged = td.get_backend() == "gloo" and any(t.is_cuda for t, _ in list(sends) + list(recvs))
+
+    # the wire carries bytes: a recording's int16 samples travel as their bytes (the NCCL
+    # process group refuses int16 tensors; the view is the same memory, received in place)
+    def wire(t):
+        return t if t.dtype in (torch.uint8, torch.int8) else t.view(torch.uint8)
+    sends = [(wire(t), p) for t, p in sends]
+    recvs = [(wire(t), p) for t, p in recvs]
     if not staged:
-        # RCCL moves bytes: a recording's int16 samples travel as their bytes (the NCCL
-        # process group refuses int16 tensors; the view is the same memory, received in place)
-        def wire(t):
-            return t if t.dtype in (torch.uint8, torch.int8) else t.view(torch.uint8)
-        ops = [td.P2POp(td.isend, wire(t), p) for t, p in sends] + [td.P2POp(td.irecv, wire(t), p) for t, p in recvs]
+        ops = [td.P2POp(td.isend, t, p) for t, p in sends] + [td.P2POp(td.irecv, t, p) for t, p in recvs]
         return td.batch_isend_irecv(ops) if ops else []
     hs = [(t.cpu(), p) for t, p in sends]
     hr = [(torch.empty(t.shape, dtype=t.dtype), t, p) for t, p in recvs]
