@@ -509,6 +509,8 @@ def main():
     ap.add_argument("--fed-steps", type=int, default=8,
                     help="timed steps of the C4 leg (N > 1): rank 0 feeding every rank its ensembles over RCCL")
     ap.add_argument("--no-c4-fed", action="store_true", help="skip the C4 leg when N > 1")
+    ap.add_argument("--fed-timeout", type=float, default=240.0,
+                    help="seconds after which the C4 leg is abandoned (the line is printed with its error)")
     ap.add_argument("--msc-format", choices=["bits", "packed"], default="packed",
                     help="MSC output of the timed steps: one bit per byte as the reference's deconvolve delivers it "
                          "(viterbi.cpp:240-241), or 8 bits per byte (dabgpu_pipe_set_packed; the DAB+ layer reads "
@@ -659,14 +661,6 @@ def main():
                  "cif_records": int((info["status"] >= 0).sum())}
     symbols = world * E * F * 76 * args.steps
     value = symbols / el
-    c4 = None
-    if fed:
-        pipe.close()
-        diq.free()
-        c4 = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs, fed_ph,
-                        args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
-    if rank != 0:
-        return
     # dominant kernel + its roofline.  Launches overlap in the pipeline (the next run's
     # demod starts beside the ACS and shares the SIMDs with it and the traceback), so the
     # in-pipeline spans include shared time; the dominant kernel is the one with the most
@@ -760,8 +754,6 @@ def main():
         out["delivered"] = delivered
     if sync_loss is not None:
         out["sync_loss"] = sync_loss
-    if c4 is not None:
-        out["c4_fed"] = c4
     if cpu is not None:
         t = cpu["tot"]
         out["cpu_baseline"] = {
@@ -785,7 +777,28 @@ def main():
             "rs_codewords_per_s": t["rs_cw"] / cpu["secs"],
             "realtime_ensembles": cpu["value"] / RT_SYMBOLS,
         }
-    print(json.dumps(out))
+    if fed:
+        # the C4 leg last (its RCCL communicator would slow the rank-local legs), under a
+        # watchdog: a transfer that never completes must not cost the line -- every rank
+        # leaves after --fed-timeout seconds, rank 0 printing the line with the leg's error
+        import threading
+
+        def abandon():
+            if rank == 0:
+                out["c4_fed"] = {"error": f"no result within {args.fed_timeout:g} s: the leg was abandoned"}
+                print(json.dumps(out), flush=True)
+            sys.stdout.flush()
+            os._exit(0)
+        guard = threading.Timer(args.fed_timeout, abandon)
+        guard.daemon = True
+        guard.start()
+        pipe.close()
+        diq.free()
+        out["c4_fed"] = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs,
+                                   fed_ph, args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
+        guard.cancel()
+    if rank == 0:
+        print(json.dumps(out))
 
 
 def c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs, fed_ph, fmt, steps,
