@@ -782,8 +782,11 @@ def main():
         # watchdog: a transfer that never completes must not cost the line -- every rank
         # leaves after --fed-timeout seconds, rank 0 printing the line with the leg's error
         import threading
+        once = threading.Lock()          # the line is printed once: by the leg or by the watchdog
 
         def abandon():
+            if not once.acquire(blocking=False):
+                return
             if rank == 0:
                 out["c4_fed"] = {"error": f"no result within {args.fed_timeout:g} s: the leg was abandoned"}
                 print(json.dumps(out), flush=True)
@@ -794,9 +797,12 @@ def main():
         guard.start()
         pipe.close()
         diq.free()
-        out["c4_fed"] = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs,
-                                   fed_ph, args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
+        c4 = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs,
+                        fed_ph, args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
+        if not once.acquire(blocking=False):
+            time.sleep(3600)             # the watchdog fired meanwhile: it prints and exits
         guard.cancel()
+        out["c4_fed"] = c4
     if rank == 0:
         print(json.dumps(out))
 
