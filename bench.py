@@ -526,6 +526,9 @@ def main():
                     help="timed steps (per acquisition mode) in which one stream every 2 steps loses sync (an "
                          "interferer over 1.5 frames: findIndex fails, goto notSynced) -- the price of a sync loss, "
                          "with the null search inside the run and in the background (DABGPU_CTL_ACQ_ASYNC)")
+    ap.add_argument("--c5-steps", type=int, default=12,
+                    help="timed steps of the C5 leg (BASELINE configs[4], 16 ensembles x 16 DAB+ subchannels) run "
+                         "after the C3 measurement at N = 1, reported as c5 in the same line (0: skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     args = ap.parse_args()
@@ -653,6 +656,17 @@ def main():
         k0 = ck + 1 + args.solo_steps + deliv_steps
         sync_loss = sync_loss_leg(dabamd, ctx, pipe, step, k0, args.sync_loss_steps, E, F, stride, diq, dist,
                                   el / args.steps * 1e3, args.iq_format)
+    c5 = None
+    if args.c5_steps > 0 and args.workload == "c3" and world == 1 and dist is None:
+        # BASELINE configs[4] in the same run (its own pipeline, after every C3 leg: never timed with
+        # them; the C3 pipeline and its streams are released first -- no C4 leg at N = 1)
+        pipe.close()
+        diq.free()
+        try:
+            c5 = c5_leg(dabamd, Ensemble, ctx, args.c5_steps, max(args.warmup, 3), F, args.cfo, args.iq_format,
+                        args.msc_format, threads)
+        except Exception as e:                          # noqa: BLE001 -- reported in the line
+            c5 = {"error": repr(e)[:300]}
     sf_ok = None
     if dp is not None:
         info = dp[0]
@@ -754,6 +768,8 @@ def main():
         out["delivered"] = delivered
     if sync_loss is not None:
         out["sync_loss"] = sync_loss
+    if c5 is not None:
+        out["c5"] = c5
     if cpu is not None:
         t = cpu["tot"]
         out["cpu_baseline"] = {
@@ -805,6 +821,69 @@ def main():
         out["c4_fed"] = c4
     if rank == 0:
         print(json.dumps(out))
+
+
+def c5_leg(dabamd, Ensemble, ctx, steps, warmup, F, cfo, iq_format, msc_format, threads, seed0=7000):
+    """BASELINE configs[4] beside the headline: 16 ensembles x 16 DAB+ subchannels (64 kbps
+    EEP-3A) -- FIC + MSC Viterbi, superframe sync, RS(120,110), AU CRC -- on this GPU, with
+    the streams resident in HBM as in the main leg; `steps` timed steps after `warmup`, then
+    one step whose FIC, MSC and superframes of ensemble 0 are checked against the
+    transmitted bits.  The same measurement as `bench.py --workload c5`, fewer steps."""
+    subch, E, desc = WORKLOADS["c5"]
+    fmt_code, bps, _ = FORMATS[iq_format]
+    P = period_frames(F, True)
+    ens = Ensemble(F * (warmup + steps + 1) + 1, subch=subch, snr_db=30.0, cfo_hz=cfo, amplitude=AMPLITUDE)
+    stride = ens.length
+    diq = ctx.buf(E * stride * bps)
+    pipe = None
+    try:
+        truth = ens.generate_period(seed0, P, truth=True)
+        truth.pop("iq")
+        for g0 in range(0, E, 8):
+            n = min(8, E - g0)
+            per = ens.period_many(n, seed0=seed0 + g0, period=P, threads=threads)
+            for e in range(n):
+                raw = to_raw(per[e], iq_format)
+                for p, q, m in ens.stream_pieces(P):
+                    diq.upload_at(raw[2 * q:2 * (q + m)], ((g0 + e) * stride + p) * bps)
+                del raw
+            del per
+        subs = [dabamd.Subch(s[0], s[1], s[2], s[3], 0 if s[4] else 1, dabamd.SUBCH_DABPLUS if s[5] else 0)
+                for s in subch]
+        pipe = dabamd.Pipeline(ctx, E, F, subs)
+        pipe.set_iq_format(fmt_code)
+        if msc_format == "packed":
+            pipe.set_packed(True)
+        pipe.acquire(diq, stride, [0] * E, [stride] * E)
+
+        def step(download=False):
+            r = pipe.run(diq, stride, [stride] * E, download=download)
+            return r, pipe.dabplus(download=download)
+        for _ in range(warmup):
+            step()
+        pipe.sync()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            step()
+        pipe.sync()
+        el = time.perf_counter() - t0
+        st0 = pipe.state(0)
+        (fic, crc, msc, valid), dp = step(download=True)
+        if pipe.packed:
+            msc = np.unpackbits(msc, axis=-1)
+        check = check_step(truth, P, st0, pipe.state(0), fic, crc, msc, valid, subch)
+        info = dp[0]
+        done = info["status"] == 3
+        check["superframes"] = int(done.sum())
+        check["au_crc_pass"] = int(sum(bin(int(x)).count("1") for x in info["au_crc_ok"][done]))
+        check["cif_records"] = int((info["status"] >= 0).sum())
+    finally:
+        if pipe is not None:
+            pipe.close()
+        diq.free()
+    return {"value": E * F * 76 * steps / el, "unit": "symbols/s", "ms_per_step": el / steps * 1e3, "steps": steps,
+            "warmup": warmup, "workload": desc, "ensembles": E, "frames_per_step": F,
+            "dabplus_subchannels": E * len(subch), "checked_step": check}
 
 
 def c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs, fed_ph, fmt, steps,
