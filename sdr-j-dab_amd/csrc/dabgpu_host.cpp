@@ -854,9 +854,15 @@ struct dabgpu_pipe {
     int32_t *si_d = nullptr;
     int16_t *corr_d = nullptr, *snr_d = nullptr;
     float *fc_d = nullptr, *fcpart_d = nullptr;
-    int32_t *slots_d = nullptr;
-    int64_t *cif0_d = nullptr;       // [2][S] per back-end stream: CIF index of each stream's first CIF slot
-    int32_t *ncif_d = nullptr;       // [2][S] CIFs each stream delivered in the run
+    // the back end's per-run descriptors, one block per back-end stream (parity), uploaded
+    // with ONE copy per run (each runtime copy is a kernel of its own on the back-end
+    // stream, ~6 us, in front of the ACS): [S] int64 CIF index of each stream's first CIF
+    // slot | [S] int32 CIFs each stream delivered | [S * F] int32 FIC ring slots
+    uint8_t *desc_d = nullptr;
+    size_t desc_sz = 0;
+    int64_t *cif0_dev(int par) const { return (int64_t *)(desc_d + par * desc_sz); }
+    int32_t *ncif_dev(int par) const { return (int32_t *)(desc_d + par * desc_sz + 8 * (size_t)S); }
+    int32_t *slots_dev(int par) const { return (int32_t *)(desc_d + par * desc_sz + 12 * (size_t)S); }
     uint32_t *dec_d[2] = {nullptr, nullptr};   // Viterbi decisions, per back-end stream
     size_t dec_sz = 0;
     int64_t dec_fic_off = 0;                    // FIC decisions: words after the MSC's
@@ -867,10 +873,12 @@ struct dabgpu_pipe {
     int32_t *h_si = nullptr;
     float2 *h_fc = nullptr;
     int16_t *h_snr = nullptr;
-    // pinned staging of the back end's per-run uploads (CIF counters, FIC slots), one
-    // half per back-end stream; ev_copy[par] marks the uploads done before reuse
-    int64_t *h_cif0 = nullptr;
-    int32_t *h_ncif = nullptr, *h_slots = nullptr;
+    // pinned staging of the descriptor blocks (desc_d's layout), one per back-end
+    // stream; ev_copy[par] marks the upload done before reuse
+    uint8_t *h_desc = nullptr;
+    int64_t *h_cif0(int par) const { return (int64_t *)(h_desc + par * desc_sz); }
+    int32_t *h_ncif(int par) const { return (int32_t *)(h_desc + par * desc_sz + 8 * (size_t)S); }
+    int32_t *h_slots(int par) const { return (int32_t *)(h_desc + par * desc_sz + 12 * (size_t)S); }
     hipEvent_t ev_copy[2] = {nullptr, nullptr};
     bool copy_rec[2] = {false, false};
     // the back-end streams' own error words (the front end's is the context's): the
@@ -1061,22 +1069,19 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     A((void **)&p->snr_d, sizeof(int16_t) * SF);
     A((void **)&p->fc_d, sizeof(float2) * SF);
     A((void **)&p->fcpart_d, sizeof(float2) * SF * kMaxChunks);
+    p->desc_sz = (12 * (size_t)p->S + 4 * (size_t)SF + 15) / 16 * 16;
     if (!rc && (hipHostMalloc((void **)&p->h_frames, sizeof(dabgpu_frame) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_si, sizeof(int32_t) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_fc, sizeof(float2) * SF, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_snr, sizeof(int16_t) * SF, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&p->h_cif0, sizeof(int64_t) * p->S * 2, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&p->h_ncif, sizeof(int32_t) * p->S * 2, hipHostMallocDefault) != hipSuccess ||
-                hipHostMalloc((void **)&p->h_slots, sizeof(int32_t) * SF * 2, hipHostMallocDefault) != hipSuccess ||
+                hipHostMalloc((void **)&p->h_desc, 2 * p->desc_sz, hipHostMallocDefault) != hipSuccess ||
                 hipHostMalloc((void **)&p->h_berr, sizeof(int32_t) * 2, hipHostMallocDefault) != hipSuccess))
         rc = fail(DABGPU_E_NOMEM, "pipe pinned staging");
     A((void **)&p->berr_d, sizeof(int32_t) * 2);
     if (!rc && (hipMemset(p->berr_d, 0, sizeof(int32_t) * 2) != hipSuccess)) rc = fail(DABGPU_E_HIP, "pipe error words");
     if (!rc) p->h_berr[0] = p->h_berr[1] = 0;
     if (const char *e = getenv("DABGPU_NO_SPECULATE")) p->speculate = !(e[0] == '1');
-    A((void **)&p->slots_d, sizeof(int32_t) * SF * 2);
-    A((void **)&p->cif0_d, sizeof(int64_t) * p->S * 2);
-    A((void **)&p->ncif_d, sizeof(int32_t) * p->S * 2);
+    A((void **)&p->desc_d, 2 * p->desc_sz);
     // MSC decisions, then the FIC's (both jobs of one run decode in one launch)
     const int64_t msc_words = p->NSUB > 0 ? dec_bytes(SF * 4 * p->NSUB, p->max_nbits) / 4 : 0;
     p->dec_fic_off = msc_words;
@@ -1165,13 +1170,13 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
     for (void *x : {(void *)p->acq_jobs_d, (void *)p->acq_res_d})
         if (x) (void)hipFree(x);
     if (p->ficprof_d) (void)hipFree(p->ficprof_d);
-    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_cif0,
-                    (void *)p->h_ncif, (void *)p->h_slots, (void *)p->h_berr})
+    for (void *h : {(void *)p->h_frames, (void *)p->h_si, (void *)p->h_fc, (void *)p->h_snr, (void *)p->h_desc,
+                    (void *)p->h_berr})
         if (h) (void)hipHostFree(h);
     if (p->sf_sparse_d) (void)hipFree(p->sf_sparse_d);
     for (void *x : {(void *)p->ring, (void *)p->prof_d, (void *)p->inv_d, (void *)p->substart_d, (void *)p->frames_d, (void *)p->si_d,
-                    (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->slots_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
-                    (void *)p->cif0_d, (void *)p->ncif_d, (void *)p->berr_d,
+                    (void *)p->corr_d, (void *)p->snr_d, (void *)p->fc_d, (void *)p->fcpart_d, (void *)p->desc_d, (void *)p->dec_d[0], (void *)p->dec_d[1],
+                    (void *)p->berr_d,
                     (void *)p->dp_sub_d, (void *)p->dp_br_d, (void *)p->dp_ring_d, (void *)p->dp_state_d, (void *)p->dp_code_d,
                     (void *)p->dp_cand_d, (void *)p->disp_d, (void *)p->substart_bad_d})
         if (x) (void)hipFree(x);
@@ -1598,22 +1603,17 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
         // staging half is reused only once its previous uploads have executed)
         if (p->copy_rec[par]) HIPCHK(hipEventSynchronize(p->ev_copy[par]));
         for (int s = 0; s < S; s++) {
-            p->h_cif0[(size_t)par * S + s] = p->st[s].cif_count;
-            p->h_ncif[(size_t)par * S + s] = 4 * dn[s];
+            p->h_cif0(par)[s] = p->st[s].cif_count;
+            p->h_ncif(par)[s] = 4 * dn[s];
         }
-        HIPCHK(hipMemcpyAsync(p->cif0_d + (size_t)par * S, p->h_cif0 + (size_t)par * S, sizeof(int64_t) * S,
-                              hipMemcpyHostToDevice, bs));
-        HIPCHK(hipMemcpyAsync(p->ncif_d + (size_t)par * S, p->h_ncif + (size_t)par * S, sizeof(int32_t) * S,
+        if (fic_bits) memcpy(p->h_slots(par), slots.data(), sizeof(int32_t) * S * F);
+        // one upload of the block (the FIC slots only when the FIC is decoded)
+        HIPCHK(hipMemcpyAsync(p->cif0_dev(par), p->h_cif0(par), 12 * (size_t)S + (fic_bits ? 4 * (size_t)S * F : 0),
                               hipMemcpyHostToDevice, bs));
         VitJob JF, JM;
         memset(&JF, 0, sizeof JF);
         memset(&JM, 0, sizeof JM);
-        int32_t *slots_d = p->slots_d + (size_t)par * S * F;
-        if (fic_bits) {
-            memcpy(p->h_slots + (size_t)par * S * F, slots.data(), sizeof(int32_t) * S * F);
-            HIPCHK(hipMemcpyAsync(slots_d, p->h_slots + (size_t)par * S * F, sizeof(int32_t) * S * F,
-                                  hipMemcpyHostToDevice, bs));
-        }
+        int32_t *slots_d = p->slots_dev(par);
         HIPCHK(hipEventRecord(p->ev_copy[par], bs));
         p->copy_rec[par] = true;
         if (fic_bits) {
@@ -1646,8 +1646,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
             JM.nsub = p->NSUB;
             JM.ncif = 4 * F;
             JM.ring = p->R;
-            JM.cif0s = p->cif0_d + (size_t)par * S;
-            JM.ncifs = p->ncif_d + (size_t)par * S;
+            JM.cif0s = p->cif0_dev(par);
+            JM.ncifs = p->ncif_dev(par);
             JM.sub_start = p->inject_bounds ? p->substart_bad_d : p->substart_d;
             JM.out = msc_bits;
             JM.out_stride = msc_stride;
@@ -1853,8 +1853,8 @@ int dabgpu_pipe_dabplus(dabgpu_pipe *p, uint8_t *sf_bytes, int32_t sf_stride, da
     J.nsub = p->NSUB;
     J.ndp = p->NDP;
     J.nstreams = p->S;
-    J.cif0s = p->cif0_d + (size_t)p->cur * p->S;
-    J.ncifs = p->ncif_d + (size_t)p->cur * p->S;
+    J.cif0s = p->cif0_dev(p->cur);
+    J.ncifs = p->ncif_dev(p->cur);
     J.dp_sub = p->dp_sub_d;
     J.dp_br = p->dp_br_d;
     J.ring = p->dp_ring_d;
