@@ -916,6 +916,7 @@ struct dabgpu_pipe {
     hipStream_t vs[2] = {nullptr, nullptr};
     int cur = 0;                                // back-end stream of the last run
     hipEvent_t ev_front = nullptr, ev_back[2] = {nullptr, nullptr}, ev_dp = nullptr;
+    bool ev_front_demod = false;     // ev_front marks this pass's demod (the speculative back end's gate)
     bool dp_rec = false;
     bool back_rec[2] = {false, false};
     hipEvent_t ev_acs[2] = {nullptr, nullptr};  // run r's ACS done (the ring's last reader)
@@ -1372,6 +1373,16 @@ static int pipe_front_pass(dabgpu_pipe *p, const void *iq, int64_t stride, const
         aux.fmt = p->iq_fmt;
         HIPCHK(launch_demod(c->stream, iq, p->frames_d, n, kChunks, c->T, (int16_t *)p->ring, nullptr, p->fcpart_d, general, aux));
         HIPCHK(prof_mark(p, DABGPU_STAGE_DEMOD, false));
+#ifndef DABGPU_BACK_AFTER_PUBLISH
+        // the speculative back end (after_launch, queued below) waits for the demod only:
+        // the publish feeds the host, not the decoders -- one kernel and its dispatch off
+        // the ACS's critical path.  The publish is still launched first, so the ACS's waves
+        // do not take the slot it needs before the host can read the pass.
+        if (after_launch) {
+            HIPCHK(hipEventRecord(p->ev_front, c->stream));
+            p->ev_front_demod = true;
+        }
+#endif
         // the host's values and the error word straight into pinned memory (no copies)
         HIPCHK(launch_front_publish(c->stream, p->fcpart_d, kChunks, n, (float *)p->fc_d, (float *)p->h_fc, p->si_d,
                                     p->h_si, p->snr_d, p->h_snr, c->err, c->h_err));
@@ -1582,6 +1593,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
     p->last_info.assign((size_t)S * F, dabgpu_frame_info());
     p->last_msc = nullptr;
     if (p->profiling == 1) p->ev_rec.clear();   // modes 2, 3 accumulate over runs
+    p->ev_front_demod = false;
     // at most one run of overlap: run r-2's ACS, the last reader of the ring slots this
     // run's demod reuses, must be done (not its traceback, FIC CRC and DAB+ layer: waiting
     // for those held the demod back from the slots the ACS's last waves leave free --
@@ -1662,7 +1674,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
         // works; only the decoders wait for it.  (Measured: launching run r's traceback
         // beside run r+1's ACS instead of beside run r+1's demod is 2 % slower -- the ACS
         // loses more than the demod gains.)
-        HIPCHK(hipEventRecord(p->ev_front, c->stream));
+        if (!p->ev_front_demod) HIPCHK(hipEventRecord(p->ev_front, c->stream));
+        p->ev_front_demod = false;
         HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
         if (fic_bits && do_msc) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
