@@ -343,6 +343,16 @@ def cpu_quota():
         return None
 
 
+def gen_threads(world):
+    """synthesis threads per rank: the job's CPU share (the cgroup quota when one is set, else
+    OMP_NUM_THREADS, else the affinity set) split over the ranks of this node, at most 16 --
+    8 ranks x 16 threads on a 16-core share would time-slice 8x"""
+    q = cpu_quota()
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    share = int(q) if q is not None else (omp if omp > 0 else len(os.sched_getaffinity(0)))
+    return max(1, min(16, share // max(world, 1)))
+
+
 def cpu_cores():
     """the cores the workers run on: the process's affinity set, capped at the box's CPU
     share (OMP_NUM_THREADS, which the GPU box sets to its share, and the cgroup quota) --
@@ -556,7 +566,7 @@ def main():
     P = period_frames(F, dabplus)
     ctx = dabamd.Context(rank_device(local))
     stride = ens.length
-    threads = min(16, os.cpu_count() or 1)
+    threads = gen_threads(world)
     fed = (world > 1 or dist is not None) and not args.no_c4_fed
     cs, _ = chunk_layout(stride, F)
     fed_ph = np.zeros((P * TF // cs, E, 2 * cs), FORMATS[args.fed_format][2]) if fed else None
@@ -807,14 +817,17 @@ def main():
                 out["c4_fed"] = {"error": f"no result within {args.fed_timeout:g} s: the leg was abandoned"}
                 print(json.dumps(out), flush=True)
             sys.stdout.flush()
-            os._exit(0)
+            os._exit(3)                  # non-zero on every rank: a hung leg is a failed run
         guard = threading.Timer(args.fed_timeout, abandon)
         guard.daemon = True
         guard.start()
         pipe.close()
         diq.free()
-        c4 = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs,
-                        fed_ph, args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
+        try:
+            c4 = c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus, P, cs,
+                            fed_ph, args.fed_format, args.fed_steps, truth, seed0, args.msc_format)
+        except Exception as e:           # noqa: BLE001 -- recorded in the line, printed once below
+            c4 = {"error": f"rank {rank}: {e!r}"[:300]}
         if not once.acquire(blocking=False):
             time.sleep(3600)             # the watchdog fired meanwhile: it prints and exits
         guard.cancel()
@@ -1090,11 +1103,13 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
                      "frames_decoded": int(frames), "frames_loss_free": E * F * steps,
                      "resyncs": int(sum(x.resyncs for x in st)), "acquiring_at_end": int(sum(x.acquiring for x in st))}
     pipe.sync()
-    pipe.control(dabamd.CTL_ACQ_SYNC)
+    pipe.control(dabamd.CTL_ACQ_ASYNC)                     # the engine's default again
     res["base_ms_per_step"] = base_ms
-    res["note"] = ("one stream every 2 steps loses sync (interferer over 1.5 frames, findIndex fails); sync: the run "
-                   "waits for its null search (k_acquire); async: the search runs in the background and that stream "
-                   "rejoins a later run (its frames delivered later, frame for frame the same)")
+    res["default_mode"] = "async"
+    res["note"] = ("one stream every 2 steps loses sync (interferer over 1.5 frames, findIndex fails); sync "
+                   "(DABGPU_CTL_ACQ_SYNC, the reference's order): the run waits for its null search (k_acquire); "
+                   "async (DABGPU_CTL_ACQ_ASYNC, the engine's default since round 6): the search runs in the background "
+                   "and that stream rejoins a later run (its frames delivered later, frame for frame the same)")
     return res
 
 

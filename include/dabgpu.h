@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DABGPU_ABI_VERSION 5
+#define DABGPU_ABI_VERSION 6
 
 /* error codes */
 #define DABGPU_OK          0
@@ -200,13 +200,22 @@ int dabgpu_ofdm_sync_demod(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_fram
 /* The kernels' NCO: oscillatorTable[first .. first+n-1] as the front-end kernels
  * compute it (float2 into out_d) -- for checking it against the table exhaustively. */
 int dabgpu_nco_eval(dabgpu_ctx *ctx, int32_t first, int32_t n, float *out_d);
-/* Test hook of the fused demod's NCO (getSamples' v *= oscillatorTable[localPhase],
- * ofdm-processor.cpp:76-81,202-226): dabgpu_ofdm_demod with `chunks` workgroups per
+/* Test hook of the fused demod's NCO and FFT (getSamples' v *= oscillatorTable[localPhase],
+ * ofdm-processor.cpp:76-81,202-226; fft.cpp:53-121): the demod with `chunks` workgroups per
  * frame (1: one recurrence over all 75 symbols, as the pipeline runs C3) that also writes
  * every data symbol's mixed FFT input, mix_d[out_slot][75][2048] cf32 (the samples
- * [T_g, T_s) of symbol l after the NCO), for comparison with the reference's table. */
-int dabgpu_ofdm_demod_mix(dabgpu_ctx *ctx, const float *iq_d, const dabgpu_frame *frames_d, int n, int chunks,
-                          float *mix_d, int16_t *softbits_d);
+ * [T_g, T_s) of symbol l after the NCO), and that FFT's output, spec_d[out_slot][75][2048]
+ * in natural bin order, both in absolute units (format's scale taken out, exactly), for
+ * comparison with the reference's table and with the transform restated.
+ *   start_index_d == NULL: the operator form (dabgpu_ofdm_demod: cf32 in, frames give
+ *     block0 / lp_data, int16 soft bits [out_slot][75][3072] into softbits_d);
+ *   start_index_d != NULL: the streaming pipeline's instantiation -- findIndex on the
+ *     window (threshold `level`, as dabgpu_ofdm_sync_demod), samples read as `format`
+ *     (DABGPU_IQ_F32 / S16 / U8) and converted in the loads, RING8 soft-bit bytes
+ *     (ibits + 127, [out_slot][75][3072]) into softbits_d. */
+int dabgpu_ofdm_demod_mix(dabgpu_ctx *ctx, const void *iq_d, int format, const dabgpu_frame *frames_d, int n,
+                          int chunks, int16_t level, int32_t *start_index_d, float *mix_d, float *spec_d,
+                          void *softbits_d);
 
 /* One symbol at a time (the reference's ofdmDecoder call pattern, ofdm-decoder.cpp:
  * 85-190), samples already mixed by the caller: kind 0 = block 0 (samples_d holds
@@ -360,18 +369,21 @@ int dabgpu_pipe_frame_info(dabgpu_pipe *p, dabgpu_frame_info *info_h);
  *   DABGPU_CTL_SCAN_ON/OFF  set_scanMode(bool) (:507-509): count No_Signal_Found
  *   DABGPU_CTL_RESYNC       drop sync: the next run searches the null symbol again from
  *                           the stream's current position (goto notSynced)
- *   DABGPU_CTL_ACQ_ASYNC    (stream ignored) a stream that needs the null search -- a sync
- *                           loss, ofdm-processor.cpp:354-357 -- gets it in the background on
- *                           a low-priority stream while the run goes on without it; the first
+ *   DABGPU_CTL_ACQ_ASYNC    (default since ABI 6; stream ignored) a stream that needs the null
+ *                           search after it had been synchronised -- a sync loss,
+ *                           ofdm-processor.cpp:354-357 -- gets it in the background on a
+ *                           low-priority stream while the run goes on without it; the first
  *                           run after the search finished continues that stream from where it
  *                           found the null (its frames are the same, delivered later: it
  *                           decodes fewer than n_frames in the runs it misses, with
- *                           DABGPU_OK).  iq_d must stay valid until the search ends
+ *                           DABGPU_OK).  A stream's first search (before any frame) stays
+ *                           inside the run.  iq_d must stay valid until the search ends
  *                           (dabgpu_stream_state.acquiring, or dabgpu_pipe_acquire_wait).
  *                           dabgpu_pipe_sync does not wait for a background search; the
  *                           other control ops do (its result is applied first, so the
  *                           control is the last word)
- *   DABGPU_CTL_ACQ_SYNC     (default) the run waits for the search and delivers n_frames
+ *   DABGPU_CTL_ACQ_SYNC     the reference's order: the run waits for every search and
+ *                           delivers n_frames (a one-ensemble caller loses nothing by it)
  *   DABGPU_CTL_INJECT_BOUNDS fault injection (stream ignored): the next run's MSC decoder
  *                           is handed a subchannel offset past the soft-bit ring; its
  *                           kernels refuse it (erasures read instead: the depunctured

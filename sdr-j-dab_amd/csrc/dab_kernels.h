@@ -47,6 +47,8 @@ struct DemodAux {
     int32_t disp_token;     // the symbol disp receives (ofdmDecoder's displayToken, 2 by default)
     float2 *mix;            // test hook (dabgpu_ofdm_demod_mix): [out_slot][75][T_u] the NCO-mixed
                             // FFT input of every data symbol, as the demod's FFT sees it
+    float2 *spec;           // with mix: [out_slot][75][T_u] that FFT's output, natural bin order
+                            // (both in absolute units: the recorded formats' scale taken out)
 };
 // The pipeline's soft-bit ring holds each ibits value v as the byte v + 127: processToken's
 // values are (int16_t)(q * 127.0) with |q| <= 1 (ofdm-decoder.cpp:188-189; a 0/0 gives 0),

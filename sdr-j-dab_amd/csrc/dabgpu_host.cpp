@@ -647,15 +647,24 @@ int dabgpu_get_snr(dabgpu_ctx *c, const float *spectrum, int16_t *snr) {
     HIPCHK(launch_snr(c->stream, spectrum, snr));
     return 0;
 }
-int dabgpu_ofdm_demod_mix(dabgpu_ctx *c, const float *iq, const dabgpu_frame *fr, int n, int chunks, float *mix,
-                          int16_t *soft) {
-    if (!c || !iq || !fr || !mix || !soft || n < 0 || chunks < 1 || chunks > NSYM) return fail(DABGPU_E_ARG, "bad args");
+int dabgpu_ofdm_demod_mix(dabgpu_ctx *c, const void *iq, int format, const dabgpu_frame *fr, int n, int chunks,
+                          int16_t level, int32_t *si, float *mix, float *spec, void *soft) {
+    if (!c || !iq || !fr || !mix || !spec || !soft || n < 0 || chunks < 1 || chunks > NSYM) return fail(DABGPU_E_ARG, "bad args");
+    if (format != DABGPU_IQ_F32 && format != DABGPU_IQ_S16 && format != DABGPU_IQ_U8) return fail(DABGPU_E_ARG, "format %d", format);
+    if (!si && format != DABGPU_IQ_F32) return fail(DABGPU_E_UNSUP, "the operator form reads cf32");
     void *part = nullptr;
     int rc = scratch(c, SC_FC, sizeof(float2) * (size_t)n * chunks, &part);
     if (rc) return rc;
     DemodAux aux{};
     aux.mix = (float2 *)mix;
-    HIPCHK(launch_demod(c->stream, iq, fr, n, chunks, c->T, soft, nullptr, (float *)part, true, aux));
+    aux.spec = (float2 *)spec;
+    aux.fmt = format;
+    if (si) {                                          // the pipeline's instantiation: findIndex + RING8
+        aux.si = si;
+        aux.level = level;
+        aux.ring8 = 1;
+    }
+    HIPCHK(launch_demod(c->stream, iq, fr, n, chunks, c->T, (int16_t *)soft, nullptr, (float *)part, true, aux));
     return 0;
 }
 int dabgpu_nco_eval(dabgpu_ctx *c, int32_t first, int32_t n, float *out) {
@@ -930,9 +939,10 @@ struct dabgpu_pipe {
     bool packed = false;             // MSC output 8 bits per byte (dabgpu_pipe_set_packed)
     int iq_fmt = DABGPU_IQ_F32;      // sample format of the streams (dabgpu_pipe_set_iq_format)
     int disp_token = 2;              // the display feed's symbol (ofdm-decoder.cpp:61 displayToken)
-    // background null search (DABGPU_CTL_ACQ_ASYNC): a stream that loses sync is searched
-    // on its own low-priority stream while the others keep decoding; its results are
-    // taken by the first dabgpu_pipe_run after they arrive
+    // background null search (DABGPU_CTL_ACQ_ASYNC, the default since round 6): a stream
+    // that loses sync after an acquisition is searched on its own low-priority stream while
+    // the others keep decoding; its results are taken by the first dabgpu_pipe_run after
+    // they arrive (set true by dabgpu_pipe_create)
     bool acq_async = false;
     hipStream_t as = nullptr;
     hipEvent_t ev_acq = nullptr;
@@ -1014,6 +1024,21 @@ extern "C" {
 int dabgpu_rs_decode(dabgpu_ctx *c, const uint8_t *in, int n, uint8_t *out, int16_t *ret) {
     if (!c || !in || !out || !ret || n < 0) return fail(DABGPU_E_ARG, "bad args");
     HIPCHK(launch_rs(c->stream, in, n, c->dptab, out, ret));
+    return 0;
+}
+
+// the background null search's stream (lowest priority), event and buffers
+static int acq_async_setup(dabgpu_pipe *p) {
+    if (p->as) return 0;
+    int lo = 0, hi = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(hipStreamCreateWithPriority(&p->as, hipStreamNonBlocking, lo));
+    HIPCHK(hipEventCreateWithFlags(&p->ev_acq, hipEventDisableTiming));
+    HIPCHK(hipMalloc((void **)&p->acq_jobs_d, sizeof(AcqJob) * p->S));
+    HIPCHK(hipMalloc((void **)&p->acq_res_d, sizeof(AcqResult) * p->S));
+    HIPCHK(hipHostMalloc((void **)&p->h_acq, sizeof(AcqResult) * p->S, hipHostMallocDefault));
+    HIPCHK(hipHostMalloc((void **)&p->h_acq_jobs, sizeof(AcqJob) * p->S, hipHostMallocDefault));
+    p->acquiring.assign(p->S, 0);
     return 0;
 }
 
@@ -1144,6 +1169,9 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
             hipMemset(p->ring, RING8_BIAS, (size_t)p->S * p->R * FRAME_SOFT) != hipSuccess)
             rc = fail(DABGPU_E_HIP, "pipe init copy failed");
     }
+    // the default re-acquisition mode: a stream that loses sync is searched in the
+    // background (DABGPU_CTL_ACQ_ASYNC; DABGPU_CTL_ACQ_SYNC restores the in-run search)
+    if (!rc && !(rc = acq_async_setup(p))) p->acq_async = true;
     if (rc) {
         dabgpu_pipe_destroy(p);
         return rc;
@@ -1671,7 +1699,13 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
             JM.dec_nch = dec_chunks(p->max_nbits);
         }
         // the small uploads above run on the back-end stream while the front end still
-        // works; only the decoders wait for it.  (Measured: launching run r's traceback
+        // works; only the decoders wait for it.
+        // What the back end may read of the front end's output: the soft-bit ring (p->ring,
+        // written by the demod) and the host-built descriptors uploaded on bs above -- never
+        // what k_front_publish writes (fc_d, si_d, snr_d, the error word): ev_front may mark
+        // the demod alone (ev_front_demod), before the publish.  A back-end reader of those
+        // must wait for an event recorded after the publish (DABGPU_BACK_AFTER_PUBLISH).
+        // (Measured: launching run r's traceback
         // beside run r+1's ACS instead of beside run r+1's demod is 2 % slower -- the ACS
         // loses more than the demod gains.)
         if (!p->ev_front_demod) HIPCHK(hipEventRecord(p->ev_front, c->stream));
@@ -1749,17 +1783,24 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
     // symbol from where it is and continues (goto notSynced, ofdm-processor.cpp:354-357).
     // Every pass either commits a frame or moves a stream past samples, so this ends.
     for (int it = 0; it < 64 * F + 64; it++) {
-        std::vector<int> who;
-        for (int s = 0; s < S; s++)
-            if (!cur[s].synced && done[s] < F && !(p->acq_async && p->acquiring[s])) who.push_back(s);
-        int found = 0;
-        if (p->acq_async) {
-            // in the background: this run goes on without those streams (one batch in flight)
-            if (!who.empty() && !p->acq_inflight)
-                if (int rc = acquire_streams_async(p, iq, stride, n_avail, who, cur)) return bail(rc);
-        } else if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) {
-            return bail(rc);
+        // streams that need the null search: in the background (DABGPU_CTL_ACQ_ASYNC, the
+        // default) those that lost sync after an acquisition -- this run goes on without
+        // them, one batch in flight; inside the run (the reference's order) the others: a
+        // stream's first search (it has no frames to decode before it) and, with
+        // DABGPU_CTL_ACQ_SYNC, every search
+        std::vector<int> who, bg;
+        for (int s = 0; s < S; s++) {
+            if (cur[s].synced || done[s] >= F) continue;
+            if (p->acq_async && cur[s].acquisitions > 0) {
+                if (!p->acquiring[s]) bg.push_back(s);
+            } else {
+                who.push_back(s);
+            }
         }
+        int found = 0;
+        if (!bg.empty() && !p->acq_inflight)
+            if (int rc = acquire_streams_async(p, iq, stride, n_avail, bg, cur)) return bail(rc);
+        if (int rc = acquire_streams(p, iq, stride, n_avail, who, cur, found)) return bail(rc);
         bool progress = false, lost = false;
         std::function<int()> after;
         if (spec && it == 0 && found == 0)
@@ -1777,7 +1818,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
     }
     bool all = true;
     for (int s = 0; s < S; s++) {
-        if (done[s] != F && !(p->acq_async && (p->acquiring[s] || !cur[s].synced))) all = false;
+        if (done[s] != F && !(p->acq_async && cur[s].acquisitions > 0 && (p->acquiring[s] || !cur[s].synced))) all = false;
         cur[s].frames_run = done[s];
     }
     std::vector<int32_t> slot((size_t)S * F, -1);
@@ -1967,17 +2008,7 @@ int dabgpu_pipe_control(dabgpu_pipe *p, int stream, int op) {
             p->acq_async = false;
             return 0;
         }
-        if (!p->as) {
-            int lo = 0, hi = 0;
-            HIPCHK(hipDeviceGetStreamPriorityRange(&lo, &hi));
-            HIPCHK(hipStreamCreateWithPriority(&p->as, hipStreamNonBlocking, lo));
-            HIPCHK(hipEventCreateWithFlags(&p->ev_acq, hipEventDisableTiming));
-            HIPCHK(hipMalloc((void **)&p->acq_jobs_d, sizeof(AcqJob) * p->S));
-            HIPCHK(hipMalloc((void **)&p->acq_res_d, sizeof(AcqResult) * p->S));
-            HIPCHK(hipHostMalloc((void **)&p->h_acq, sizeof(AcqResult) * p->S, hipHostMallocDefault));
-            HIPCHK(hipHostMalloc((void **)&p->h_acq_jobs, sizeof(AcqJob) * p->S, hipHostMallocDefault));
-            p->acquiring.assign(p->S, 0);
-        }
+        if (int rc = acq_async_setup(p)) return rc;
         p->acq_async = true;
         return 0;
     }

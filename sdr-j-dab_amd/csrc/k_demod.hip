@@ -112,16 +112,25 @@ __device__ __forceinline__ float quad_bfly(float v, float sign) {
 // VALU instead of a DPP move and an fma, the same single rounding.  The s_nop 1 is the two
 // wait states a DPP read needs after the VALU write of its source (the hazard recognizer
 // does not look inside inline assembly).
+// (GFX9 DPP syntax and wait states: gfx942 / gfx950 only; elsewhere -- and in the host
+// pass -- the same value as a DPP move and an fma.  Not volatile: the asm has no side
+// effect beyond its output, so the compiler may schedule around it.)
 template <int M>
 __device__ __forceinline__ float quad_bfly_s(float v, float sign) {
+#if defined(__gfx950__) || defined(__gfx942__)
     float r;
     if constexpr (M == 2)
-        asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1"
-                     : "=v"(r) : "v"(v), "v"(sign), "0"(v));
+        asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "=v"(r) : "v"(v), "v"(sign), "0"(v));
     else
-        asm volatile("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
-                     : "=v"(r) : "v"(v), "v"(sign), "0"(v));
+        asm("s_nop 1\n\tv_fmac_f32_dpp %0, %1, %2 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1"
+            : "=v"(r) : "v"(v), "v"(sign), "0"(v));
     return r;
+#else
+    constexpr int ctrl = M == 2 ? 0x4E : 0xB1;
+    const float p = __int_as_float(__builtin_amdgcn_update_dpp(__float_as_int(v), __float_as_int(v), ctrl, 0xF, 0xF, true));
+    return fmaf(p, sign, v);
+#endif
 }
 
 // v[m] *= oscillatorTable[localPhase] sample by sample (ofdm-processor.cpp:186-201).
@@ -596,9 +605,16 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
             if constexpr (DUMP) {                      // test hook: the FFT's input, mixed
                 float2 *mp = aux.mix + ((int64_t)fr.out_slot * NSYM + (l - 1)) * TU;
 #pragma unroll
-                for (int m = 0; m < 8; m++) mp[t + 256 * m] = a[m];
+                for (int m = 0; m < 8; m++) mp[t + 256 * m] = make_float2(a[m].x * Fmt::unscale, a[m].y * Fmt::unscale);
             }
             fft2048_wg<true>(a, ex, tw, t);
+            if constexpr (DUMP) {                      // ... and its output (tau and the scale taken out: exact)
+                float2 *sp = aux.spec + ((int64_t)fr.out_slot * NSYM + (l - 1)) * TU;
+                const int b0 = bin0_of(t);
+                const float s = tw.tau * Fmt::unscale;
+#pragma unroll
+                for (int k = 0; k < 8; k++) sp[b0 + 64 * k] = make_float2(a[k].x * s, a[k].y * s);
+            }
             if (aux.disp && l == aux.disp_token) {     // the display token's carriers (ofdm-decoder.cpp:197-205)
                 float2 *dp = aux.disp + (int64_t)fr.out_slot * K;
                 const int b0 = bin0_of(t);
@@ -937,9 +953,18 @@ hipError_t launch_demod(hipStream_t st, const void *iq, const dabgpu_frame *fr, 
         if (aux.si) { if (general) DEMOD_GO(true, true, R, F, false); else DEMOD_GO(false, true, R, F, false); } \
         else { if (general) DEMOD_GO(true, false, R, F, false); else DEMOD_GO(false, false, R, F, false); }     \
     } while (0)
-    if (aux.mix) {                                     // the NCO test hook: operator form only
-        if (!general || aux.si || aux.ring8 || aux.fmt != DABGPU_IQ_F32) return hipErrorInvalidValue;
-        DEMOD_GO(true, false, false, DABGPU_IQ_F32, true);
+    if (aux.mix) {                                     // the NCO / FFT test hook (GEN kernels only)
+        if (!general || !aux.spec) return hipErrorInvalidValue;
+        if (!aux.si) {                                 // the operator form: cf32 in, int16 out
+            if (aux.ring8 || aux.fmt != DABGPU_IQ_F32) return hipErrorInvalidValue;
+            DEMOD_GO(true, false, false, DABGPU_IQ_F32, true);
+        } else {                                       // the pipeline's form: findIndex, RING8, any format
+            if (!aux.ring8) return hipErrorInvalidValue;
+            if (aux.fmt == DABGPU_IQ_S16) DEMOD_GO(true, true, true, DABGPU_IQ_S16, true);
+            else if (aux.fmt == DABGPU_IQ_U8) DEMOD_GO(true, true, true, DABGPU_IQ_U8, true);
+            else if (aux.fmt == DABGPU_IQ_F32) DEMOD_GO(true, true, true, DABGPU_IQ_F32, true);
+            else return hipErrorInvalidValue;
+        }
     } else if (aux.ring8) {                            // the pipeline's RING8 ring, any sample format
         if (aux.fmt == DABGPU_IQ_S16) DEMOD_GS(true, DABGPU_IQ_S16);
         else if (aux.fmt == DABGPU_IQ_U8) DEMOD_GS(true, DABGPU_IQ_U8);

@@ -99,7 +99,7 @@ def lib() -> C.CDLL:
             "dabgpu_ofdm_symbol": ([vp, vp, i32, vp, vp], i32),
             "dabgpu_get_snr": ([vp, vp, vp], i32),
             "dabgpu_nco_eval": ([vp, i32, i32, vp], i32),
-            "dabgpu_ofdm_demod_mix": ([vp, vp, vp, i32, i32, vp, vp], i32),
+            "dabgpu_ofdm_demod_mix": ([vp, vp, i32, vp, i32, i32, C.c_int16, vp, vp, vp, vp], i32),
             "dabgpu_pipe_set_iq_format": ([vp, i32], i32),
             "dabgpu_pipe_acquire_wait": ([vp], i32),
             "dabgpu_pipe_set_display_token": ([vp, i32], i32),
@@ -488,24 +488,39 @@ class Context:
                     b.free()
 
 
-    def demod_mix(self, iq: DevBuf, frames: Sequence[Frame], chunks: int = 1):
+    def demod_mix(self, iq: DevBuf, frames: Sequence[Frame], chunks: int = 1, fmt: int = None, level: int = 3,
+                  with_spec: bool = False):
         """dabgpu_ofdm_demod_mix: the fused demod's NCO-mixed FFT input of every data
-        symbol, complex64 [n, 75, 2048] (samples [T_g, T_s) of symbol l after getSamples'
-        NCO), and the int16 soft bits [n, 75, 3072]; `chunks` workgroups per frame"""
+        symbol, float32 [n, 75, 2048, 2] (samples [T_g, T_s) of symbol l after getSamples'
+        NCO), and the soft bits; `chunks` workgroups per frame.
+        fmt None: the operator form (cf32 in, frames give block0; int16 soft bits [n, 75, 3072]).
+        fmt IQ_F32 / IQ_S16 / IQ_U8: the pipeline's instantiation (findIndex on each frame's
+        window, samples read in that format, RING8 soft bytes [n, 75, 3072] u8); the start
+        indices are returned too.  Returns (mix, soft) -- (mix, soft, start_index) with fmt --
+        and the FFT output [n, 75, 2048] complex64 (natural bins) last when with_spec."""
         n = len(frames)
         fa = (Frame * n)(*frames)
         dfr = DevBuf(self, C.sizeof(fa)).upload(np.frombuffer(fa, dtype=np.uint8))
         dm = self.buf(8 * n * NSYM * 2048)
-        ds = self.buf(2 * n * NSYM * SYMBITS)
+        dp = self.buf(8 * n * NSYM * 2048)
+        sync = fmt is not None
+        ds = self.buf((1 if sync else 2) * n * NSYM * SYMBITS)
+        dsi = self.buf(4 * n) if sync else None
         try:
-            _chk(lib().dabgpu_ofdm_demod_mix(self.h, iq.ptr, dfr.ptr, n, chunks, dm.ptr, ds.ptr), "ofdm_demod_mix")
+            _chk(lib().dabgpu_ofdm_demod_mix(self.h, iq.ptr, IQ_F32 if fmt is None else fmt, dfr.ptr, n, chunks, level,
+                                             dsi.ptr if sync else None, dm.ptr, dp.ptr, ds.ptr), "ofdm_demod_mix")
             mix = dm.download(np.float32, (n, NSYM, 2048, 2))
-            soft = ds.download(np.int16, (n, NSYM, SYMBITS))
+            soft = ds.download(np.uint8 if sync else np.int16, (n, NSYM, SYMBITS))
+            out = (mix, soft) + ((dsi.download(np.int32, n),) if sync else ())
+            if with_spec:
+                sp = dp.download(np.float32, (n, NSYM, 2048, 2))
+                out += (sp[..., 0] + 1j * sp[..., 1],)
             self.check()
-            return mix, soft
+            return out
         finally:
-            for b in (dfr, dm, ds):
-                b.free()
+            for b in (dfr, dm, dp, ds, dsi):
+                if b is not None:
+                    b.free()
 
     def nco_eval(self, first: int = 0, n: int = 2048000) -> np.ndarray:
         """oscillatorTable[first:first+n] as the front-end kernels compute it
@@ -564,6 +579,7 @@ class Pipeline:
         self.msc_stride = (self.msc_stride + 15) // 16 * 16
         self.msc_stride_packed = self.msc_stride // 8        # bytes per codeword with set_packed
         self.packed = False
+        self.iq_format = IQ_F32                              # dabgpu_pipe_set_iq_format's default
         # consecutive runs decode concurrently on two back-end streams (dabgpu.h,
         # dabgpu_pipe_sync): outputs alternate between two buffer sets
         self._outs = [(ctx.buf(n_streams * n_frames * 4 * 768), ctx.buf(n_streams * n_frames * 12),

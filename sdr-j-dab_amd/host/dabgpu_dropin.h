@@ -395,8 +395,13 @@ public:
     void stopDumping();
     // the display symbol of the decoder this processor drives (ofdmDecoder::set_displayToken,
     // ofdm-decoder.h:50; the reference's ofdmProcessor owns its ofdmDecoder): 1..75, from
-    // the next frame on
-    void set_displayToken(int16_t t) { displayToken_ = t; }
+    // the next frame on.  A value outside 1..75 selects no symbol: in the reference such a
+    // token never matches blkno (ofdm-decoder.cpp:192-195), so the display feed stops and the
+    // decode goes on -- the setter keeps the last valid token and turns the feed off
+    void set_displayToken(int16_t t) {
+        if (t >= 1 && t <= 75) { displayToken_ = t; displayOff_ = false; }
+        else displayOff_ = true;
+    }
     int64_t frames() const { return frames_.load(); }
     static constexpr int32_t spectrumSize = 32768;          // bufferSize (ofdm-processor.cpp:97)
 private:
@@ -423,6 +428,7 @@ private:
     std::atomic<SNDFILE *> dumpSnd_{nullptr};
     int16_t dumpScaler_ = 512;
     std::atomic<int16_t> displayToken_{ofdmDecoder::defaultDisplayToken};
+    std::atomic<bool> displayOff_{false};
     // observables state
     int64_t last_block0_ = -1;
     int32_t avgTokenLength_ = 196608, tokenCount_ = 0;

@@ -309,6 +309,9 @@ void ofdmProcessor::run() {                                        // ofdm-proce
         dabgpu_pipe *p;
         ~PipeGuard() { dabgpu_pipe_destroy(p); }
     } guard{pipe};
+    // one ensemble: nothing decodes beside a null search, so it runs inside the run, in the
+    // reference's order (the engine's default background search pays off for batches)
+    chk(dabgpu_pipe_control(pipe, -1, DABGPU_CTL_ACQ_SYNC), "dabgpu_pipe_control");
     if (iqBuffer_) chk(dabgpu_pipe_set_display(pipe, 1), "dabgpu_pipe_set_display");
     // the stream in HBM: samples [base, end) of the device's sample sequence in one of
     // two buffers (the kernels index absolute sample numbers from buf - 2 * base);
@@ -362,8 +365,9 @@ void ofdmProcessor::run() {                                        // ofdm-proce
         last_run = end;
         // decode every frame the samples so far allow, one per pipeline run
         for (;;) {
-            const int16_t token = displayToken_.load();
-            if (iqBuffer_) chk(dabgpu_pipe_set_display_token(pipe, token), "dabgpu_pipe_set_display_token");
+            // token 0 (display off: an out-of-range set_displayToken) matches no blkno below
+            const int16_t token = displayOff_.load() ? 0 : displayToken_.load();
+            if (iqBuffer_ && token) chk(dabgpu_pipe_set_display_token(pipe, token), "dabgpu_pipe_set_display_token");
             const float *iq = (const float *)bufs[cur].get() - 2 * base;
             win_ = (const float *)bufs[cur].get();
             win_base_ = base;

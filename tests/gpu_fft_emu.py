@@ -1,16 +1,26 @@
-"""ANALYSIS TOOL (not test infrastructure, not product): the GPU demod's FFT
-(k_demod.hip fft2048_wg: radix-8 / W2048 twiddles, radix-8 / W256, radix-8 / W32 and the
-quad's DPP radix-4, fma twiddle products) restated in numpy float32, operation for
-operation, so its rounding can be compared with other fp32 transforms on the CPU
-(tools/soft_floor.py).  It reproduces the GPU's soft values (e.g. the max |dq| of
-test_demod_nco_matches_oracle at -4201 Hz, 2.646e-5, to the digit)."""
+"""TEST INFRASTRUCTURE (a checker, not product): the GPU demod's FFT (k_demod.hip
+fft2048_wg: radix-8 / W2048 twiddles, radix-8 / W256, radix-8 / W32 and the quad's DPP
+radix-4, fma twiddle products) restated in numpy float32, operation for operation.
+tests/test_gpu_parity.py::test_demod_fft_equals_restated_transform pins it bit for bit to
+the fused demod's spectra; tools/soft_floor.py compares its rounding with other fp32
+transforms on the CPU."""
 import numpy as np
 f32 = np.float32
 W = np.exp(-2j*np.pi*np.arange(2048)/2048)
 Wr = W.real.astype(f32); Wi = W.imag.astype(f32)
 C = f32(0.70710678118654752440)
-def fmaf(a,b,c):  # float32 fma emulated in double (product exact)
-    return (a.astype(np.float64)*b.astype(np.float64) + c.astype(np.float64)).astype(f32)
+def fmaf(a,b,c):
+    """float32 fma, exactly: the product is exact in double; the double sum s = RN(p + c)
+    rounds to the float RN(p + c) unless s is itself a float midpoint (double rounding),
+    where the sign of the sum's error e (TwoSum) decides"""
+    p = np.asarray(a, np.float64) * np.asarray(b, np.float64)
+    c = np.asarray(c, np.float64)
+    s = p + c
+    bp = s - c
+    e = (p - bp) + (c - (s - bp))
+    mid = (s.view(np.uint64) & np.uint64(0x1FFFFFFF)) == np.uint64(0x10000000)
+    s = np.where(mid & (e != 0), np.nextafter(s, np.where(e > 0, np.inf, -np.inf)), s)
+    return s.astype(f32)
 def cmul(ar, ai, wr, wi):
     return fmaf(ar, wr, -(ai*wi)), fmaf(ar, wi, ai*wr)
 def dft8(ar, ai):  # ar, ai: lists of 8 arrays

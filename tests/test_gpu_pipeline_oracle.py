@@ -85,7 +85,7 @@ def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs, fmt):
     F = 4
     iqs = _gen(MIXED, F * runs + 1, [31, 32], snr, cfo, fmt)
     refs = orc.decode_streams(iqs, F * runs, MIXED)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, MIXED, soft_streams=(0, 1), iq_format=fmt)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, MIXED, soft_streams=(0, 1), iq_format=fmt, acq="sync")
     stats = [pc.compare(gpu[s], refs[s], MIXED) for s in range(2)]
     print(f"snr {snr} cfo {cfo} fmt {fmt}:", stats)
     _check(stats, (snr, cfo, fmt))
@@ -155,7 +155,8 @@ def test_pipeline_dropout_reacquires_like_reference(ctx, fmt):
     PRS correlation is flat, so findIndex fails -- Max < 3 * mean): the stream goes back
     to the null search from where it is (goto notSynced), which finds the next null once
     the signal returns -- frame for frame the oracle's ofdmProcessor::run, inside ONE
-    pipeline run"""
+    pipeline run (DABGPU_CTL_ACQ_SYNC: the reference's in-run search; the engine's default
+    searches in the background, test_pipeline_background_reacquisition_like_reference)"""
     from dabamd.synth import Ensemble
     sub = MIXED[:2]
     F, runs = 4, 3
@@ -173,7 +174,7 @@ def test_pipeline_dropout_reacquires_like_reference(ctx, fmt):
     iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
     iq = pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt)
     ref = orc.decode_stream(iq, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt)
+    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt, acq="sync")
     st = pc.compare(gpu[0], ref, sub)
     print("dropout:", st, [(x.resyncs, x.acquisitions, x.frames_run) for x in gpu[0]["states"]])
     _check([st], "dropout")
@@ -212,11 +213,12 @@ def test_pipeline_digital_silence_like_reference(ctx, fmt):
 
 @FMTS
 def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
-    """DABGPU_CTL_ACQ_ASYNC: stream 0 loses sync in a dropout (as above); its null search
-    runs in the background while stream 1 keeps decoding n_frames per run, and the runs
-    after the search continue stream 0 from the null it found -- both streams' frames
-    (placement, FIC, MSC, soft bits) equal the oracle's ofdmProcessor::run frame for frame,
-    stream 0's delivered later"""
+    """The engine's default re-acquisition (DABGPU_CTL_ACQ_ASYNC, round 6), and the same
+    mode set explicitly: stream 0 loses sync in a dropout (as above); its null search runs
+    in the background while stream 1 keeps decoding n_frames per run, and the runs after
+    the search continue stream 0 from the null it found -- both streams' frames (placement,
+    FIC, MSC, soft bits) equal the oracle's ofdmProcessor::run frame for frame, stream 0's
+    delivered later"""
     from dabamd.synth import Ensemble
     sub = MIXED[:2]
     F, runs = 4, 7
@@ -232,18 +234,19 @@ def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
     iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
     iqs = [pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt), pc.quantize(g1["iq"], fmt)]
     refs = orc.decode_streams(iqs, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), acq_async=True, iq_format=fmt)
-    runs0 = [(x.frames_run, x.acquiring, x.resyncs) for x in gpu[0]["states"]]
-    print("background re-acquisition:", runs0)
-    assert all(x.frames_run == F for x in gpu[1]["states"])          # stream 1 never waits
-    assert any(fr < F for fr, _, _ in runs0)                          # stream 0 missed runs while searching
-    assert gpu[0]["states"][-1].resyncs >= 1 and gpu[0]["states"][-1].acquisitions >= 2
-    for s in range(2):
-        st = pc.compare(gpu[s], refs[s], sub)
-        print("stream", s, st)
-        _check([st], ("background", s))
-    st0 = pc.compare(gpu[0], refs[0], sub)
-    assert st0["frames"] > 4                   # frames after the dropout were decoded too
+    for acq in (None, "async"):
+        gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), acq=acq, iq_format=fmt)
+        runs0 = [(x.frames_run, x.acquiring, x.resyncs) for x in gpu[0]["states"]]
+        print("background re-acquisition", acq or "(default)", runs0)
+        assert all(x.frames_run == F for x in gpu[1]["states"])          # stream 1 never waits
+        assert any(fr < F for fr, _, _ in runs0)                          # stream 0 missed runs while searching
+        assert gpu[0]["states"][-1].resyncs >= 1 and gpu[0]["states"][-1].acquisitions >= 2
+        for s in range(2):
+            st = pc.compare(gpu[s], refs[s], sub)
+            print("stream", s, st)
+            _check([st], ("background", acq, s))
+        st0 = pc.compare(gpu[0], refs[0], sub)
+        assert st0["frames"] > 4                   # frames after the dropout were decoded too
 
 
 def test_background_search_flag_clears_without_a_run(ctx):

@@ -1,12 +1,12 @@
-"""The soft values' fp32 floor, on the CPU: for the six cases
+"""The soft values' fp32 floor, on the CPU: for the seven cases
 (transmitted offset / NCO phase) of test_demod_nco_matches_oracle (the same streams, frames and NCO-mixed samples),
 max |q - q_oracle| over every soft value of 3 frames x 75 symbols when the FFT is
-  gpu-emu      the GPU demod's radix-8/8/8/4 transform (tools/gpu_fft_emu.py)
+  gpu-emu      the GPU demod's radix-8/8/8/4 transform (tests/gpu_fft_emu.py)
   radix-4      the oracle's fp32 radix-4 Stockham transform (orc_fft2048_f32)
   r2-dit/dif   the oracle's fp32 radix-2 DIT / DIF transforms
 against the oracle's double-precision FFT rounded to float; plus each transform's relative
 rms error on random input and the count of soft values off by more than 1e-5.
-usage: python tools/soft_floor.py > profiles/r05_soft_floor.txt"""
+usage: python tools/soft_floor.py > profiles/r06_soft_floor.txt"""
 import os
 import sys
 
@@ -17,7 +17,7 @@ sys.path[:0] = [os.path.join(ROOT, "sdr-j-dab_amd"), os.path.join(ROOT, "tests")
 import dabamd                                    # noqa: E402
 import gpu_fft_emu                               # noqa: E402
 import oracle_py as orc                          # noqa: E402
-from test_gpu_parity import NCO_CASES, _case_off, _cfo_frames, _nco_mix   # noqa: E402
+from test_gpu_parity import NCO_CASES, _cfo_frames, _nco_mix   # noqa: E402
 
 osc = dabamd.host_table(dabamd.TABLE_OSC)
 mp = dabamd.host_table(dabamd.TABLE_MAPPER).astype(np.int64)
@@ -49,12 +49,12 @@ def main():
           "   ".join(f"{k} {rel(ffts(x, v)):.3e}" for k, v in KINDS.items()))
     print()
     print("max |q - q_oracle| (unweighted) per case (transmitted offset / NCO phase + data-symbol phase offset),")
-    print("and [soft values off by > 1e-5]; the last row is the smeared case with the +17 data offset (not a test case):")
+    print("and [soft values off by > 1e-5], the rms, and round 6's criterion against the radix-4:")
     print(f"  {'cfo/nco':>14} " + " ".join(f"{k:>20}" for k in ["gpu-emu"] + list(KINDS)))
-    cases = [(c, n, _case_off(n)) for c, n in NCO_CASES] + [(0.0, 12345, 17)]
+    cases = NCO_CASES
     for cfo, nco, off in cases:
         g, xs, frs = _cfo_frames(cfo, nco=nco, phase_b_off=off)
-        res = {k: [0.0, 0] for k in ["gpu-emu"] + list(KINDS)}
+        res = {k: [0.0, 0, 0.0, 0] for k in ["gpu-emu"] + list(KINDS)}
         for fr in frs:
             pa = np.arange(fr.block0, fr.block0 + 2048)
             blk = _nco_mix(xs[pa], pa, fr.lp_window, fr.phase_a, fr.window, osc)
@@ -73,7 +73,14 @@ def main():
                     d = np.abs(q_of(X[l], X[l - 1]) - qd)
                     res[k][0] = max(res[k][0], float(d.max()))
                     res[k][1] += int((d > 1e-5).sum())
+                    res[k][2] += float(np.sum(d.astype(np.float64) ** 2))
+                    res[k][3] += d.size
         print(f"  {cfo:6.0f}/{nco if nco is not None else round(cfo):6.0f}+{off:<2d}" + " ".join(f"{v[0]:11.3e} [{v[1]:5d}]" for v in res.values()))
+        rms = {k: np.sqrt(v[2] / v[3]) for k, v in res.items()}
+        g, r4 = res["gpu-emu"], res["radix-4"]
+        ok = (rms["gpu-emu"] <= 1.1 * rms["radix-4"], g[1] <= 2 * r4[1], g[0] <= max(1e-5, 2 * r4[0]))
+        print(f"  {'':16} rms " + " ".join(f"{v:11.3e}        " for v in rms.values()) +
+              f" criterion vs radix-4 (rms <= 1.1x, count <= 2x, max <= max(1e-5, 2x)): {ok}")
 
 
 if __name__ == "__main__":
