@@ -1,6 +1,7 @@
 """TEST INFRASTRUCTURE (a checker, not product): the GPU demod's FFT (k_demod.hip
 fft2048_wg: radix-8 / W2048 twiddles, radix-8 / W256, radix-8 / W32 and the quad's DPP
-radix-4, fma twiddle products) restated in numpy float32, operation for operation.
+radix-4, fma twiddle products, and the fma the compiler contracts inside the radix-8
+butterfly) restated in numpy float32, operation for operation.
 tests/test_gpu_parity.py::test_demod_fft_equals_restated_transform pins it bit for bit to
 the fused demod's spectra; tools/soft_floor.py compares its rounding with other fp32
 transforms on the CPU."""
@@ -28,16 +29,27 @@ def dft8(ar, ai):  # ar, ai: lists of 8 arrays
     for j in range(4):
         br[j]=ar[j]+ar[j+4]; bi[j]=ai[j]+ai[j+4]
         br[j+4]=ar[j]-ar[j+4]; bi[j+4]=ai[j]-ai[j+4]
-    br[5], bi[5] = C*(br[5]+bi[5]), C*(bi[5]-br[5])
+    # the W8^1 / W8^3 products: b5 = C s5, b7 = (C s7r, -C s7i)
+    s5r, s5i = br[5]+bi[5], bi[5]-br[5]
+    s7r, s7i = bi[7]-br[7], br[7]+bi[7]
+    p7r, p7i = C*s7r, -(C*s7i)
     br[6], bi[6] = bi[6], -br[6]
-    br[7], bi[7] = C*(bi[7]-br[7]), -C*(br[7]+bi[7])
     dr=[None]*8; di=[None]*8
-    for h in (0,4):
-        dr[h]=br[h]+br[h+2]; di[h]=bi[h]+bi[h+2]
-        dr[h+1]=br[h+1]+br[h+3]; di[h+1]=bi[h+1]+bi[h+3]
-        dr[h+2]=br[h]-br[h+2]; di[h+2]=bi[h]-bi[h+2]
-        tr=br[h+1]-br[h+3]; ti=bi[h+1]-bi[h+3]
-        dr[h+3]=ti; di[h+3]=-tr
+    h=0
+    dr[h]=br[h]+br[h+2]; di[h]=bi[h]+bi[h+2]
+    dr[h+1]=br[h+1]+br[h+3]; di[h+1]=bi[h+1]+bi[h+3]
+    dr[h+2]=br[h]-br[h+2]; di[h+2]=bi[h]-bi[h+2]
+    tr=br[h+1]-br[h+3]; ti=bi[h+1]-bi[h+3]
+    dr[h+3]=ti; di[h+3]=-tr
+    # h = 4: b5 +- b7 -- the compiler contracts (k_demod.hip builds with fp-contract=fast):
+    # the b5 product is fused, fma(C, s5, +-b7), the b7 product rounded first (found on the
+    # GPU's own spectra, test_demod_fft_equals_restated_transform)
+    Cv = lambda a: np.full_like(a, C)
+    dr[4]=br[4]+br[6]; di[4]=bi[4]+bi[6]
+    dr[5]=fmaf(Cv(s5r), s5r, p7r); di[5]=fmaf(Cv(s5i), s5i, p7i)
+    dr[6]=br[4]-br[6]; di[6]=bi[4]-bi[6]
+    tr=fmaf(Cv(s5r), s5r, -p7r); ti=fmaf(Cv(s5i), s5i, -p7i)
+    dr[7]=ti; di[7]=-tr
     o_r=[None]*8; o_i=[None]*8
     pairs=[(0,4,0,1),(2,6,2,3),(1,5,4,5),(3,7,6,7)]
     for a,b,x,y in pairs:
