@@ -102,6 +102,12 @@ def dist_setup(n_gpus):
         # leg's transfers, after the rank-local legs)
         global _CTL
         _CTL = td.new_group(backend="gloo") if backend == "nccl" else None
+        if backend == "nccl" and os.environ.get("DAB_RCCL_EARLY") == "1":
+            # A/B hook (tools/rccl_overhead.sh): create the RCCL communicator before the
+            # rank-local legs, as round 5's first N > 1 path did
+            t = torch.ones(1, device=f"cuda:{local}")
+            td.all_reduce(t)
+            torch.cuda.synchronize()
     return rank, local, world, dist
 
 
