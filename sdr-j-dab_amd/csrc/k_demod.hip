@@ -185,8 +185,9 @@ struct DemodTw {
 // fma.  For DQPSK the sign cancels (X_l conj(X_{l-1}) with both scaled by the same tau: the
 // same products, bit for bit), and |X| is unchanged; the callers that need X itself use
 // SIGNED = false.
-template <bool SIGNED = false>
-__device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const DemodTw &tw, int t) {
+// passes 1-3 of fft2048_wg: afterwards thread t (quad g = t >> 2, t'' = t & 3) holds in a[k3]
+// the radix-4 input t'' of group (g, k3), twiddled by W32^(t'' k3)
+__device__ __forceinline__ void fft2048_p123(float2 (&a)[8], float2 *ex, const DemodTw &tw, int t) {
     // pass 1
     dft8(a);
 #pragma unroll
@@ -214,6 +215,10 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
 #pragma unroll
         for (int k = 1; k < 8; k++) a[k] = cmulw(a[k], tw.w3[(k - 1) * 4 + tq]);
     }
+}
+template <bool SIGNED = false>
+__device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const DemodTw &tw, int t) {
+    fft2048_p123(a, ex, tw, t);
     // pass 4: radix-4 over the quad's t''; lane t'' ends with K'' = brev2(t'')
 #pragma unroll
     for (int k = 0; k < 8; k++) {
@@ -229,6 +234,76 @@ __device__ __forceinline__ void fft2048_wg(float2 (&a)[8], float2 *ex, const Dem
     }
 }
 
+
+// The data symbols' FFT tail (round 6, k_demod_wg): instead of pass 4's DPP radix-4 across
+// the quad, pass 3's outputs go through LDS inside the quad that produced them -- the 4
+// values t'' = 0..3 of group (g, k3) at ex[g * ZROW + 4 k3 + t''], i.e. row g, which only
+// quad g reads or writes from pass 3 on (each lane overwrites the entries it read in pass 3),
+// so the wave's own program order is all the ordering needed -- and thread t = 4 g + a takes
+// the groups (g, a) and (g, a + 4): the radix-4 over t'' in registers, with the same
+// operations as pass 4 (x0 +- x2, x1 +- x3, -j, then the sums: the spectrum bit for bit).
+// Of a group's outputs X[K''] (bin b0(g) + 64 k3 + 512 K''), K'' = 0 and 3 are carriers
+// (bins 1..511, 1536..2047), K'' = 1 only for k3 <= 3 (512..767) and K'' = 2 only for
+// k3 >= 4 (1280..1535): every thread holds exactly 6 carriers -- thread 0 the carrier at
+// bin 768 (group (0, 4), K'' = 1) in place of the DC bin -- so DQPSK and the soft bits run
+// on 6 slots, not 8 bins.
+struct Quad4 { float2 s02, d02, s13, d13; };
+__device__ __forceinline__ float2 rotmj(float2 d) { return make_float2(d.y, -d.x); }      // -j d
+__device__ __forceinline__ Quad4 r4_terms(const float2 (&x)[4]) {
+    return {cadd(x[0], x[2]), csub(x[0], x[2]), cadd(x[1], x[3]), csub(x[1], x[3])};
+}
+// X[K''] of a group: X0 = s02 + s13, X1 = d02 - j d13, X2 = s02 - s13, X3 = d02 + j d13
+__device__ __forceinline__ float2 r4_out(const Quad4 &q, int K) {
+    return K == 0 ? cadd(q.s02, q.s13) : K == 1 ? cadd(q.d02, rotmj(q.d13)) : K == 2 ? csub(q.s02, q.s13)
+                                                                             : csub(q.d02, rotmj(q.d13));
+}
+__device__ __forceinline__ void fft2048_tail(const float2 (&a)[8], float2 *ex, int t, Quad4 &qa, Quad4 &qb) {
+    const int g = t >> 2, tq = t & 3;
+    float2 *row = ex + g * ZROW;
+#pragma unroll
+    for (int k = 0; k < 8; k++) row[4 * k + tq] = a[k];
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    float2 xa[4], xb[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        xa[u] = row[4 * tq + u];
+        xb[u] = row[4 * (tq + 4) + u];
+    }
+    qa = r4_terms(xa);
+    qb = r4_terms(xb);
+}
+// the FFT bin of output (group grp = 0: k3 = a, 1: k3 = a + 4; K'') of thread t
+__device__ __forceinline__ int tail_bin(int t, int grp, int K) {
+    const int g = t >> 2, a = t & 3;
+    return (g >> 3) + 8 * (g & 7) + 64 * (a + 4 * grp) + 512 * K;
+}
+// slot j -> (group, K''): A0 A1 A3 B0 B2 B3 (thread 0: B1 for A0)
+__device__ __forceinline__ int slot_bin(int t, int j) {
+    constexpr int grp[6] = {0, 0, 0, 1, 1, 1}, kk[6] = {0, 1, 3, 0, 2, 3};
+    return (t == 0 && j == 0) ? tail_bin(t, 1, 1) : tail_bin(t, grp[j], kk[j]);
+}
+__device__ __forceinline__ void tail_slots(const Quad4 &A, const Quad4 &B, int t, float2 (&S)[6]) {
+    S[0] = r4_out(A, 0);
+    S[1] = r4_out(A, 1);
+    S[2] = r4_out(A, 3);
+    S[3] = r4_out(B, 0);
+    S[4] = r4_out(B, 2);
+    S[5] = r4_out(B, 3);
+    if (__builtin_amdgcn_readfirstlane(t) < 64) {      // wave 0 (uniform): thread 0's carrier 768
+        const float2 b1 = r4_out(B, 1);
+        if (t == 0) S[0] = b1;
+    }
+}
+// all 8 outputs (get_snr, the display feed, the test hook): X[4 grp + K''] at tail_bin(t, grp, K'')
+__device__ __forceinline__ void tail_all(const Quad4 &A, const Quad4 &B, float2 (&X)[8]) {
+#pragma unroll
+    for (int K = 0; K < 4; K++) {
+        X[K] = r4_out(A, K);
+        X[4 + K] = r4_out(B, K);
+    }
+}
 
 // twiddle tables of fft2048_wg in LDS, laid out per pass so that a wave's reads are
 // conflict-free (the values are the W2048 table's entries: W256^j = W2048^(8 j),
@@ -334,12 +409,12 @@ __device__ __forceinline__ int32_t prs_corr_wg(float2 (&a)[8], float2 *ex, const
 // (dab-constants.h:107-109).  The sums are workgroup trees (the reference adds in bin
 // order): a display value, equal to the sequential one except within float rounding
 // of a dB boundary.
-__device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R, float unscale = 1.0f) {
-    const int b0 = bin0_of(t);
+template <class BinOf>
+__device__ __forceinline__ int16_t snr_wg_b(const float2 (&a)[8], BinOf bin_of, RedLds &R, int t, float unscale) {
     float noise = 0.0f, signal = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; k++) {
-        const int b = b0 + 64 * k;
+        const int b = bin_of(k);
         const float v = hypotf(a[k].x * unscale, a[k].y * unscale);      // (a power of two: exact)
         if ((b >= 1034 && b < 1260) || (b >= 788 && b < 1014)) noise += v;
         if (b >= 1664 || b < 384) signal += v;
@@ -351,6 +426,10 @@ __device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R
     const float db_s = 20 * log10f((signal / 768 + 1) / (float)256);
     const float db_n = 20 * log10f((noise + 1) / (float)256);
     return (int16_t)(db_s - db_n);
+}
+__device__ __forceinline__ int16_t snr_wg(const float2 (&a)[8], int t, RedLds &R, float unscale = 1.0f) {
+    const int b0 = bin0_of(t);
+    return snr_wg_b(a, [&](int k) { return b0 + 64 * k; }, R, t, unscale);
 }
 
 // (int16_t)((double)q * 127.0) for q = RN(-re / ab1) and the same for im -- the
@@ -469,15 +548,12 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
     if (!ok && !skip && t == 0) atomicOr(T.err, KERR_FRAME);
     if (l0 <= NSYM && ok && !skip) {
         const int64_t dorg = fr.block0 + TU;           // first sample of segment B
-        // LDS stage byte address of each of this thread's 8 bins (its carrier's word, or a
-        // dump word for a bin that carries nothing), two u16 per register, and the stage
-        // words of the carrier pairs its read-back quads q = t, t + DT take
-        uint32_t cb[4], rq[2];
+        // LDS stage byte address of each of this thread's 6 carrier slots (fft2048_tail), and
+        // the stage words of the carrier pairs its read-back quads q = t, t + DT take
+        uint32_t cb[6], rq[2];
         {
-            const int b0 = bin0_of(t);
-            auto slot = [&](int k3) -> uint32_t { return (uint32_t)T.stage_of_bin[b0 + 64 * k3] * 4u; };
 #pragma unroll
-            for (int k3 = 0; k3 < 8; k3 += 2) cb[k3 >> 1] = slot(k3) | (slot(k3 + 1) << 16);
+            for (int j = 0; j < 6; j++) cb[j] = (uint32_t)T.stage_of_bin[slot_bin(t, j)] * 4u;
 #pragma unroll
             for (int i = 0; i < 2; i++) {
                 const int q = t + DT * i;
@@ -504,30 +580,37 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
         // off: byte offset from block 0; the prefetch registers hold the raw samples (8, 4
         // or 2 bytes), converted when the symbol's turn comes
         auto ld = [&](int32_t off) -> typename Fmt::raw { return Fmt::load(rin, off); };
-        // the spectra of symbols l and l - 1 alternate between A and B (the loop runs two
-        // symbols per trip), so neither is copied into the other per symbol
-        float2 A[8], B[8];
+        // the 6 carrier slots of symbols l and l - 1 alternate between A and B (the loop runs
+        // two symbols per trip), so neither is copied into the other per symbol
+        float2 A[6], B[6];
         typename Fmt::raw nx[8], ng6, ng7;
         // warm-up symbol l0 - 1 (block 0, the PRS, for the first chunk)
+        int32_t ov = (l0 * TS + t) * BPS;                     // this thread's sample 0 of symbol l
         {
             const int64_t u = fr.block0 + (int64_t)(l0 - 1) * TS;
             const int32_t o = ((l0 - 1) * TS + t) * BPS;
+            float2 x[8];
 #pragma unroll
-            for (int m = 0; m < 8; m++) B[m] = Fmt::scaled(ld(o + 256 * BPS * m));
-            if (l0 == 1) mix<GEN>(B, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
-            else mix<GEN>(B, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
-        }
-        int32_t ov = (l0 * TS + t) * BPS;                     // this thread's sample 0 of symbol l
-        ng6 = ld(ov - 512 * BPS);
-        ng7 = ld(ov - 256 * BPS);
+            for (int m = 0; m < 8; m++) x[m] = Fmt::scaled(ld(o + 256 * BPS * m));
+            if (l0 == 1) mix<GEN>(x, T.osc, ncl, fr.lp_window, fr.phase_a, u + t, fr.window);
+            else mix<GEN>(x, T.osc, ncl, fr.lp_data, fr.phase_b, u + t, dorg);
+            // symbol l0's samples in flight during the warm-up FFT
+            ng6 = ld(ov - 512 * BPS);
+            ng7 = ld(ov - 256 * BPS);
 #pragma unroll
-        for (int m = 0; m < 8; m++) nx[m] = ld(ov + 256 * BPS * m);
-        fft2048_wg<true>(B, ex, tw, t);
-        if (l0 == 1 && aux.snr) {                       // processBlock_0's get_snr (ofdm-decoder.cpp:93)
-            const int16_t v = snr_wg(B, t, red, Fmt::unscale);
-            if (t == 0) aux.snr[fi] = v;
+            for (int m = 0; m < 8; m++) nx[m] = ld(ov + 256 * BPS * m);
+            fft2048_p123(x, ex, tw, t);
+            Quad4 qa, qb;
+            fft2048_tail(x, ex, t, qa, qb);
+            tail_slots(qa, qb, t, B);
+            if (l0 == 1 && aux.snr) {                   // processBlock_0's get_snr (ofdm-decoder.cpp:93)
+                float2 X[8];
+                tail_all(qa, qb, X);
+                const int16_t v = snr_wg_b(X, [&](int k) { return tail_bin(t, k >> 2, k & 3); }, red, t, Fmt::unscale);
+                if (t == 0) aux.snr[fi] = v;
+            }
         }
-        __syncthreads();                                // pass 3 read ex: the first symbol's pass 1 writes it
+        __syncthreads();                                // the tail read ex: the first symbol's pass 1 writes it
         // NCO of segment B (round 4): thread t's samples of symbol l are n = t + 256 m, so
         // their oscillatorTable indices step by -d256 per m and by -dsym per symbol (mod
         // 2048000).  The exact e^{2 pi i ti / N} of the chunk's first sample (the factor
@@ -562,12 +645,13 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
 
             efc = nco_value(ncl, nco_mod(-(int64_t)TU * ph));
         }
-        // symbol l: a = its spectrum (computed here), P = symbol l - 1's
-        auto sym = [&](const int l, float2 (&a)[8], const float2 (&P)[8]) __attribute__((always_inline)) {
+        // symbol l: S = its 6 carrier slots (computed here), P = symbol l - 1's
+        auto sym = [&](const int l, float2 (&S)[6], const float2 (&P)[6]) __attribute__((always_inline)) {
             // this symbol's samples and its guard samples, all loaded one symbol ahead
             // (a guard load issued here would expose a full HBM latency per symbol).  The
             // loads after the chunk's last symbol are not conditional: past the frame they
             // read the buffer's out-of-range zeros, inside it a symbol nobody uses
+            float2 a[8];
 #pragma unroll
             for (int m = 0; m < 8; m++) a[m] = Fmt::scaled(nx[m]);
             const float2 g6 = Fmt::scaled(ng6), g7 = Fmt::scaled(ng7);
@@ -607,67 +691,66 @@ __global__ __launch_bounds__(DT, DEMOD_WG_PER_SIMD) void k_demod_wg(const void *
 #pragma unroll
                 for (int m = 0; m < 8; m++) mp[t + 256 * m] = make_float2(a[m].x * Fmt::unscale, a[m].y * Fmt::unscale);
             }
-            fft2048_wg<true>(a, ex, tw, t);
-            if constexpr (DUMP) {                      // ... and its output (tau and the scale taken out: exact)
-                float2 *sp = aux.spec + ((int64_t)fr.out_slot * NSYM + (l - 1)) * TU;
-                const int b0 = bin0_of(t);
-                const float s = tw.tau * Fmt::unscale;
+            fft2048_p123(a, ex, tw, t);
+            Quad4 qa, qb;
+            fft2048_tail(a, ex, t, qa, qb);
+            tail_slots(qa, qb, t, S);
+            const bool disp = aux.disp && l == aux.disp_token;
+            if (DUMP || disp) {                        // all 8 outputs: the test hook, the display feed
+                float2 X[8];
+                tail_all(qa, qb, X);
+                if constexpr (DUMP) {                  // ... the FFT's output (the scale taken out: exact)
+                    float2 *sp = aux.spec + ((int64_t)fr.out_slot * NSYM + (l - 1)) * TU;
 #pragma unroll
-                for (int k = 0; k < 8; k++) sp[b0 + 64 * k] = make_float2(a[k].x * s, a[k].y * s);
-            }
-            if (aux.disp && l == aux.disp_token) {     // the display token's carriers (ofdm-decoder.cpp:197-205)
-                float2 *dp = aux.disp + (int64_t)fr.out_slot * K;
-                const int b0 = bin0_of(t);
+                    for (int k = 0; k < 8; k++)
+                        sp[tail_bin(t, k >> 2, k & 3)] = make_float2(X[k].x * Fmt::unscale, X[k].y * Fmt::unscale);
+                }
+                if (disp) {                            // the display token's carriers (ofdm-decoder.cpp:197-205)
+                    float2 *dp = aux.disp + (int64_t)fr.out_slot * K;
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int b = b0 + 64 * k;
-                    const float s = tw.tau * Fmt::unscale;     // a power of two, signed: exact
-                    const float2 v = make_float2(a[k].x * s, a[k].y * s);
-                    if (b < K / 2) dp[b] = v;
-                    else if (b >= TU - 1 - K / 2 && b < TU - 1) dp[b - (TU - 1 - K)] = v;
+                    for (int k = 0; k < 8; k++) {
+                        const int b = tail_bin(t, k >> 2, k & 3);
+                        const float2 v = make_float2(X[k].x * Fmt::unscale, X[k].y * Fmt::unscale);
+                        if (b < K / 2) dp[b] = v;
+                        else if (b >= TU - 1 - K / 2 && b < TU - 1) dp[b - (TU - 1 - K)] = v;
+                    }
                 }
             }
-            __syncthreads();                           // pass 3's reads of ex done: st reuses it
-            // DQPSK + soft bits of the 8 bins, fast path first; the few bins whose
+            __syncthreads();                           // the tail's reads of ex done: st reuses it
+            // DQPSK + soft bits of the 6 slots, fast path first; the few carriers whose
             // truncation the fast path cannot decide (soft_fast) are redone exactly after
-            // all 8 (one divergent branch per symbol instead of one per bin)
-            // (the flag is a lane mask in SGPRs: the rare lanes recompute which bins need it)
+            // all 6 (one divergent branch per symbol instead of one per carrier)
+            // (the flag is a lane mask in SGPRs: the rare lanes recompute which need it)
             bool risky = false;
 #pragma unroll
-            for (int k = 0; k < 8; k++) {
-                const float2 r1 = cmul_conj_exact(a[k], P[k]);
+            for (int k = 0; k < 6; k++) {
+                const float2 r1 = cmul_conj_exact(S[k], P[k]);
                 // ibits = (int16_t)(q * 127.0), q = -re / ab1 (IEEE float division) and
                 // ab1 = |re| + |im| (ofdm-decoder.cpp:185-189)
                 const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                 int ir, ii;
                 risky |= soft_fast<FMT != DABGPU_IQ_F32>(r1, ab1, ir, ii);
-                const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
-                *(uint32_t *)((char *)st + addr) = spair(ir, ii);
+                *(uint32_t *)((char *)st + cb[k]) = spair(ir, ii);
             }
             if (risky) {
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const float2 r1 = cmul_conj_exact(a[k], P[k]);
+                for (int k = 0; k < 6; k++) {
+                    const float2 r1 = cmul_conj_exact(S[k], P[k]);
                     const float ab1 = fabsf(r1.x) + fabsf(r1.y);
                     int ir, ii;
-                    if (soft_fast<FMT != DABGPU_IQ_F32>(r1, ab1, ir, ii)) {
-                        const uint32_t addr = (k & 1) ? (cb[k >> 1] >> 16) : (cb[k >> 1] & 0xFFFFu);
-                        *(uint32_t *)((char *)st + addr) = spair(trunc127d(-r1.x / ab1), trunc127d(-r1.y / ab1));
-                    }
+                    if (soft_fast<FMT != DABGPU_IQ_F32>(r1, ab1, ir, ii))
+                        *(uint32_t *)((char *)st + cb[k]) = spair(trunc127d(-r1.x / ab1), trunc127d(-r1.y / ab1));
                 }
             }
             if (softf) {                               // parity tests only: the float soft values
                 float *sf = softf + ((int64_t)fr.out_slot * NSYM + (l - 1)) * SYMBITS;
-                const int b0 = bin0_of(t);
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const int c = T.carrier_of_bin[b0 + 64 * k];
-                    if (c >= 0) {
-                        const float2 r1 = cmul_conj_exact(a[k], P[k]);
-                        const float ab1 = fabsf(r1.x) + fabsf(r1.y);
-                        sf[c] = -r1.x / ab1;
-                        sf[K + c] = -r1.y / ab1;
-                    }
+                for (int k = 0; k < 6; k++) {
+                    const int c = T.carrier_of_bin[slot_bin(t, k)];
+                    const float2 r1 = cmul_conj_exact(S[k], P[k]);
+                    const float ab1 = fabsf(r1.x) + fabsf(r1.y);
+                    sf[c] = -r1.x / ab1;
+                    sf[K + c] = -r1.y / ab1;
                 }
             }
             __syncthreads();

@@ -27,6 +27,10 @@
 #include <mutex>
 #include <thread>
 
+#ifdef DABGPU_HAVE_SNDFILE
+#include <sndfile.h>          // a build with libsndfile (the reference's gui.cpp / wavfiles)
+#endif
+
 #include "dabgpu.h"
 #include "fib_processor.h"
 #include "msc_consumers.h"
@@ -296,12 +300,24 @@ private:
     int16_t new_language_ = 0, new_type_ = 0;
 };
 
-// ---- libsndfile stand-in (the .sdr dump) ---------------------------------------------
+// ---- libsndfile (the .sdr dump) -------------------------------------------------------
 // gui.cpp:861-893 opens the dump with sf_open (path, SFM_WRITE, {INPUT_RATE, 2 channels,
 // SF_FORMAT_WAV | SF_FORMAT_PCM_16}) and hands the SNDFILE* to ofdmProcessor::startDumping,
 // which writes interleaved PCM16 frames with sf_writef_short (ofdm-processor.cpp:150-157).
-// libsndfile is not in this image: this is the subset those calls use, writing the same
+// Built with -DDABGPU_HAVE_SNDFILE (and -lsndfile), dabgpu:: names libsndfile's own types
+// and calls, so the GUI's ::SNDFILE* binds to startDumping unchanged.  Without it (this
+// image has no libsndfile) a stand-in with the subset those calls use writes the same
 // RIFF/WAVE PCM16 file (the header's sizes are filled in by sf_close).
+#ifdef DABGPU_HAVE_SNDFILE
+using ::SF_INFO;
+using ::SNDFILE;
+using ::sf_close;
+using ::sf_open;
+using ::sf_writef_short;
+using ::SFM_WRITE;
+using ::SF_FORMAT_WAV;
+using ::SF_FORMAT_PCM_16;
+#else
 struct SF_INFO {
     int64_t frames;
     int samplerate, channels, format, sections, seekable;
@@ -312,6 +328,7 @@ constexpr int SF_FORMAT_WAV = 0x010000, SF_FORMAT_PCM_16 = 0x0002;
 SNDFILE *sf_open(const char *path, int mode, SF_INFO *info);   // SFM_WRITE, WAV PCM16 only (else nullptr)
 int64_t sf_writef_short(SNDFILE *f, const int16_t *ptr, int64_t frames);
 int sf_close(SNDFILE *f);
+#endif
 
 // ---- OFDM front end ----------------------------------------------------------------
 // ofdmDecoder (ofdm-decoder.cpp:37-230, ofdm-decoder.h:40-48) one symbol per call on the

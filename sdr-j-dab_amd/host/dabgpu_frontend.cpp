@@ -31,7 +31,8 @@ void setModeParameters(DabParams *p, uint8_t mode) {              // gui.cpp:136
     p->carrierDiff = 1000;
 }
 
-// ---- libsndfile stand-in -----------------------------------------------------------
+// ---- libsndfile stand-in (a build with -DDABGPU_HAVE_SNDFILE uses libsndfile itself) --
+#ifndef DABGPU_HAVE_SNDFILE
 struct SNDFILE {
     FILE *f = nullptr;
     int channels = 2, samplerate = 0;
@@ -82,6 +83,7 @@ int sf_close(SNDFILE *s) {
     delete s;
     return r;
 }
+#endif
 
 // ---- ofdmDecoder ------------------------------------------------------------------
 std::atomic<int> ofdmDecoder::iq_count{0};

@@ -74,3 +74,24 @@ def test_ringbuffer_and_sdr_dump_standin(tmp_path):
         d = np.frombuffer(w.readframes(3 * 4096), "<i2").reshape(-1, 2)
     k = np.arange(3 * 4096)
     assert np.array_equal(d[:, 0], (k - 6000).astype(np.int16)) and np.array_equal(d[:, 1], (-k).astype(np.int16))
+
+
+def test_dropin_binds_libsndfile_when_built_with_it():
+    """built with -DDABGPU_HAVE_SNDFILE the drop-ins take
+    libsndfile's own SNDFILE / SF_INFO / sf_* (the stand-in steps aside), so gui.cpp's
+    set_dumping (gui.cpp:861-893) hands its ::SNDFILE* to ofdmProcessor::startDumping
+    unchanged.  libsndfile is absent here: compiled against its API declarations
+    (tests/cpp/sndfile_api/sndfile.h), not linked."""
+    import shutil
+    import subprocess
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("no g++")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    inc = ["-I" + os.path.join(root, "tests", "cpp", "sndfile_api"), "-I" + os.path.join(root, "include"),
+           "-I" + os.path.join(root, "sdr-j-dab_amd", "host")]
+    for src in (os.path.join(root, "sdr-j-dab_amd", "host", "dabgpu_frontend.cpp"),
+                os.path.join(root, "tests", "cpp", "gui_dump_sndfile.cpp")):
+        r = subprocess.run([gxx, "-std=c++17", "-fsyntax-only", "-Wall", "-DDABGPU_HAVE_SNDFILE"] + inc + [src],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, r.stderr[-2000:]
