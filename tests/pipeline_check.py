@@ -40,17 +40,18 @@ def to_raw(iq, fmt):
 
 
 def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=(), dabplus=False, packed=False,
-               acq=None, packed_pad=0, iq_format=IQ_F32, dev_iq=None):
+               acq="sync", packed_pad=0, iq_format=IQ_F32, dev_iq=None):
     """Decode `runs` x F frames of every stream.  iqs: list of float32 IQ arrays
     (interleaved); n_avail: optional list (per run) of per-stream available sample
     counts.  iq_format: the streams go to the GPU as that recorded format (iqs must be
     representable: quantize()), read by the kernels through dabgpu_pipe_set_iq_format.
     dev_iq: (DevBuf, stride) already in HBM in that format (e.g. Context.load_recording)
     instead of uploading iqs (which then only give the stream lengths).
-    acq: the re-acquisition mode -- None, the engine's default (a stream that loses sync is
-    searched in the background, DABGPU_CTL_ACQ_ASYNC; between runs the caller waits up to
-    50 ms for a search in flight, a real-time feed's pace); "sync" (DABGPU_CTL_ACQ_SYNC: the
-    reference's in-run search, every stream delivers n_frames per run); "async" (explicit
+    acq: the re-acquisition mode -- "sync" (DABGPU_CTL_ACQ_SYNC: the reference's in-run
+    search, so every stream's frames per run are the oracle's ofdmProcessor::run's, which
+    the frame-count assertions check); "default" (the engine's default, a stream that loses
+    sync is searched in the background, DABGPU_CTL_ACQ_ASYNC; between runs the caller waits
+    up to 50 ms for a search in flight, a real-time feed's pace); "async" (explicit
     DABGPU_CTL_ACQ_ASYNC after a synchronous first acquisition, 50 ms between runs).
     Returns per stream: dict(info [frames], fic, crc, msc {cif: [nsub][nb]},
     soft {frame: [75][3072]} for soft_streams, sf {cif: [(info, bytes)...]})."""
@@ -88,7 +89,7 @@ def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=()
             na = n_avail[r] if n_avail is not None else lens
             if acq == "async" and r:
                 time.sleep(0.05)    # a background search finishes between runs (a real-time feed's pace)
-            elif acq is None and r:
+            elif acq == "default" and r:
                 t0 = time.time()
                 while any(pipe.state(s).acquiring for s in range(S)) and time.time() - t0 < 0.05:
                     time.sleep(0.001)

@@ -77,7 +77,7 @@ def test_ringbuffer_and_sdr_dump_standin(tmp_path):
 
 
 def test_dropin_binds_libsndfile_when_built_with_it():
-    """INTEGRATION.md section 5: built with -DDABGPU_HAVE_SNDFILE the drop-ins take
+    """INTEGRATION.md section 4: built with -DDABGPU_HAVE_SNDFILE the drop-ins take
     libsndfile's own SNDFILE / SF_INFO / sf_* (the stand-in steps aside), so gui.cpp's
     set_dumping (gui.cpp:861-893) hands its ::SNDFILE* to ofdmProcessor::startDumping
     unchanged.  libsndfile is absent here: compiled against its API declarations

@@ -85,7 +85,7 @@ def test_pipeline_bits_match_reference_path(ctx, snr, cfo, runs, fmt):
     F = 4
     iqs = _gen(MIXED, F * runs + 1, [31, 32], snr, cfo, fmt)
     refs = orc.decode_streams(iqs, F * runs, MIXED)
-    gpu = pc.gpu_decode(ctx, iqs, F, runs, MIXED, soft_streams=(0, 1), iq_format=fmt, acq="sync")
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, MIXED, soft_streams=(0, 1), iq_format=fmt)
     stats = [pc.compare(gpu[s], refs[s], MIXED) for s in range(2)]
     print(f"snr {snr} cfo {cfo} fmt {fmt}:", stats)
     _check(stats, (snr, cfo, fmt))
@@ -155,8 +155,9 @@ def test_pipeline_dropout_reacquires_like_reference(ctx, fmt):
     PRS correlation is flat, so findIndex fails -- Max < 3 * mean): the stream goes back
     to the null search from where it is (goto notSynced), which finds the next null once
     the signal returns -- frame for frame the oracle's ofdmProcessor::run, inside ONE
-    pipeline run (DABGPU_CTL_ACQ_SYNC: the reference's in-run search; the engine's default
-    searches in the background, test_pipeline_background_reacquisition_like_reference)"""
+    pipeline run (DABGPU_CTL_ACQ_SYNC, as every test here that counts frames: the reference's
+    in-run search; the engine's default searches in the background,
+    test_pipeline_background_reacquisition_like_reference)"""
     from dabamd.synth import Ensemble
     sub = MIXED[:2]
     F, runs = 4, 3
@@ -174,7 +175,7 @@ def test_pipeline_dropout_reacquires_like_reference(ctx, fmt):
     iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
     iq = pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt)
     ref = orc.decode_stream(iq, F * runs, sub)
-    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt, acq="sync")
+    gpu = pc.gpu_decode(ctx, [iq], F, runs, sub, soft_streams=(0,), iq_format=fmt)
     st = pc.compare(gpu[0], ref, sub)
     print("dropout:", st, [(x.resyncs, x.acquisitions, x.frames_run) for x in gpu[0]["states"]])
     _check([st], "dropout")
@@ -234,10 +235,10 @@ def test_pipeline_background_reacquisition_like_reference(ctx, fmt):
     iq[a:b, 1] = level * np.sin(ph) + rng.normal(0, level / 10, b - a)
     iqs = [pc.quantize(np.ascontiguousarray(iq.reshape(-1)), fmt), pc.quantize(g1["iq"], fmt)]
     refs = orc.decode_streams(iqs, F * runs, sub)
-    for acq in (None, "async"):
+    for acq in ("default", "async"):
         gpu = pc.gpu_decode(ctx, iqs, F, runs, sub, soft_streams=(0, 1), acq=acq, iq_format=fmt)
         runs0 = [(x.frames_run, x.acquiring, x.resyncs) for x in gpu[0]["states"]]
-        print("background re-acquisition", acq or "(default)", runs0)
+        print("background re-acquisition", acq, runs0)
         assert all(x.frames_run == F for x in gpu[1]["states"])          # stream 1 never waits
         assert any(fr < F for fr, _, _ in runs0)                          # stream 0 missed runs while searching
         assert gpu[0]["states"][-1].resyncs >= 1 and gpu[0]["states"][-1].acquisitions >= 2
