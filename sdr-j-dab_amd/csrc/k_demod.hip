@@ -257,29 +257,14 @@ __device__ __forceinline__ float2 r4_out(const Quad4 &q, int K) {
     return K == 0 ? cadd(q.s02, q.s13) : K == 1 ? cadd(q.d02, rotmj(q.d13)) : K == 2 ? csub(q.s02, q.s13)
                                                                              : csub(q.d02, rotmj(q.d13));
 }
-#ifndef TAIL_LAYOUT
-#define TAIL_LAYOUT 1
-#endif
 __device__ __forceinline__ void fft2048_tail(const float2 (&a)[8], float2 *ex, int t, Quad4 &qa, Quad4 &qb) {
     const int g = t >> 2, tq = t & 3;
     float2 *row = ex + g * ZROW;
     float2 xa[4], xb[4];
-#if TAIL_LAYOUT == 0
-    // (k3, t'') at row[4 k3 + t'']: 8 b64 stores, 4 b128 loads (4-way bank conflicts)
-#pragma unroll
-    for (int k = 0; k < 8; k++) row[4 * k + tq] = a[k];
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-    for (int u = 0; u < 4; u++) {
-        xa[u] = row[4 * tq + u];
-        xb[u] = row[4 * (tq + 4) + u];
-    }
-#else
-    // (k3, t'') at row[8 t'' + k3]: a lane's 8 values contiguous (4 b128 stores, ~2-way
-    // bank conflicts in each 16-lane group), the group reads as 8 b64 loads whose 32-lane
-    // halves hit 64 distinct banks (72 g + 16 u + 2 a words: conflict-free)
+    // (k3, t'') at row[8 t'' + k3]: a lane's 8 values contiguous (4 b128 stores), the groups
+    // read as 8 b64 loads whose 32-lane halves hit 64 distinct banks (72 g + 16 u + 2 a
+    // words).  (The layout row[4 k3 + t''] -- 8 b64 stores, 4 b128 loads -- measured the same,
+    // profiles/r06_demod_tail_ab.txt.)
     float4 *w = (float4 *)(row + 8 * tq);
 #pragma unroll
     for (int k = 0; k < 8; k += 2) w[k >> 1] = make_float4(a[k].x, a[k].y, a[k + 1].x, a[k + 1].y);
@@ -291,7 +276,6 @@ __device__ __forceinline__ void fft2048_tail(const float2 (&a)[8], float2 *ex, i
         xa[u] = row[8 * u + tq];
         xb[u] = row[8 * u + tq + 4];
     }
-#endif
     qa = r4_terms(xa);
     qb = r4_terms(xb);
 }
