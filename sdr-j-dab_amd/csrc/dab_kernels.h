@@ -203,6 +203,9 @@ hipError_t launch_acs(hipStream_t st, const VitJob &job);
 hipError_t launch_traceback(hipStream_t st, const VitJob &job);
 hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
 hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &msc, const VitJob &fic);
+hipError_t launch_acs_msc_fic_range(hipStream_t st, const VitJob &msc, const VitJob &fic, int b0, int b1, bool with_fic);
+hipError_t launch_traceback_msc_fic_range(hipStream_t st, const VitJob &msc, const VitJob &fic, int b0, int b1,
+                                          bool with_fic);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib, const uint8_t *tabs,
                            const int32_t *slots = nullptr);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);

@@ -896,6 +896,13 @@ struct dabgpu_pipe {
     int32_t *berr_d = nullptr, *h_berr = nullptr;
     // speculative back end (dabgpu_pipe_run): queued behind the first front pass
     bool speculate = true;                      // env DABGPU_NO_SPECULATE=1: off (A/B)
+    // env DABGPU_VIT_SLICES=K (A/B): the MSC Viterbi in K slices -- slice
+    // i's ACS on the back-end stream, its traceback on ts behind an event, so it reads
+    // decisions the ACS wrote moments before (<= 256 MB per slice: Infinity-Cache resident)
+    int vit_slices = 1;
+    hipStream_t ts = nullptr;
+    std::vector<hipEvent_t> ev_slice;
+    hipEvent_t ev_tb = nullptr;
     int64_t front_launches = 0, spec_runs = 0, spec_hits = 0;
     int max_nbits = 0;
     std::vector<dabgpu_frame> last_frames;   // [S][F]
@@ -1107,6 +1114,17 @@ int dabgpu_pipe_create(dabgpu_ctx *c, const dabgpu_pipe_cfg *cfg, dabgpu_pipe **
     if (!rc && (hipMemset(p->berr_d, 0, sizeof(int32_t) * 2) != hipSuccess)) rc = fail(DABGPU_E_HIP, "pipe error words");
     if (!rc) p->h_berr[0] = p->h_berr[1] = 0;
     if (const char *e = getenv("DABGPU_NO_SPECULATE")) p->speculate = !(e[0] == '1');
+    if (const char *e = getenv("DABGPU_VIT_SLICES")) p->vit_slices = std::max(1, std::min(64, atoi(e)));
+    if (!rc && p->vit_slices > 1) {
+        int lo = 0, hi = 0;
+        p->ev_slice.assign(p->vit_slices, nullptr);
+        if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess ||
+            hipStreamCreateWithPriority(&p->ts, hipStreamNonBlocking, lo) != hipSuccess ||
+            hipEventCreateWithFlags(&p->ev_tb, hipEventDisableTiming) != hipSuccess)
+            rc = fail(DABGPU_E_HIP, "slice stream");
+        for (auto &e : p->ev_slice)
+            if (!rc && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) rc = fail(DABGPU_E_HIP, "slice events");
+    }
     A((void **)&p->desc_d, 2 * p->desc_sz);
     // MSC decisions, then the FIC's (both jobs of one run decode in one launch)
     const int64_t msc_words = p->NSUB > 0 ? dec_bytes(SF * 4 * p->NSUB, p->max_nbits) / 4 : 0;
@@ -1189,6 +1207,12 @@ int dabgpu_pipe_destroy(dabgpu_pipe *p) {
                         p->ev_acs[0], p->ev_acs[1]})
         if (e) (void)hipEventDestroy(e);
     for (hipStream_t v : p->vs) if (v) (void)hipStreamDestroy(v);
+    if (p->ts) {
+        (void)hipStreamSynchronize(p->ts);
+        (void)hipStreamDestroy(p->ts);
+    }
+    for (hipEvent_t e : p->ev_slice) if (e) (void)hipEventDestroy(e);
+    if (p->ev_tb) (void)hipEventDestroy(p->ev_tb);
     if (p->as) {                                    // a background null search still running
         (void)hipStreamSynchronize(p->as);
         (void)hipStreamDestroy(p->as);
@@ -1711,7 +1735,27 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
         if (!p->ev_front_demod) HIPCHK(hipEventRecord(p->ev_front, c->stream));
         p->ev_front_demod = false;
         HIPCHK(hipStreamWaitEvent(bs, p->ev_front, 0));
-        if (fic_bits && do_msc) {
+        if (fic_bits && do_msc && p->vit_slices > 1) {
+            // the A/B form: K slices of traceback blocks; slice i's traceback on ts reads the
+            // decisions slice i's ACS has just written while slice i + 1's ACS runs
+            const int nblk = (JM.n_cw + 63) / 64, K = p->vit_slices, per = (nblk + K - 1) / K;
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
+            for (int i = 0; i * per < nblk; i++) {
+                const int b0 = i * per, b1 = std::min(nblk, b0 + per);
+                HIPCHK(launch_acs_msc_fic_range(bs, JM, JF, b0, b1, b1 == nblk));
+                HIPCHK(hipEventRecord(p->ev_slice[i], bs));
+                HIPCHK(hipStreamWaitEvent(p->ts, p->ev_slice[i], 0));
+                HIPCHK(launch_traceback_msc_fic_range(p->ts, JM, JF, b0, b1, b1 == nblk));
+            }
+            HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));
+            HIPCHK(hipEventRecord(p->ev_acs[par], bs));
+            p->acs_rec[par] = true;
+            HIPCHK(hipEventRecord(p->ev_tb, p->ts));
+            HIPCHK(hipStreamWaitEvent(bs, p->ev_tb, 0));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
+            HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
+        } else if (fic_bits && do_msc) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
             HIPCHK(launch_acs_msc_fic(bs, JM, JF));
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, false));

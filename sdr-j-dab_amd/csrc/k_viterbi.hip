@@ -994,13 +994,14 @@ __global__ __launch_bounds__(64, 8) void k_acs(VitJob J) {
     __shared__ AcsLds<1> L;
     acs_body<KIND, 1, B8>(J, xcd_order(blockIdx.x, gridDim.x), L);
 }
-// two jobs in one launch (the pipeline's MSC and FIC): blocks [0, nwa) run job A,
-// the rest job B, so B's short waves fill the SIMDs A's last waves leave idle
+// two jobs in one launch (the pipeline's MSC and FIC): blocks [0, nwa) run job A's waves
+// wa0 .. wa0 + nwa - 1, the rest job B, so B's short waves fill the SIMDs A's last waves
+// leave idle (wa0 > 0: a slice of A, DABGPU_VIT_SLICES)
 template <int KA, int KB, bool B8 = false>
-__global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa) {
+__global__ __launch_bounds__(64, 8) void k_acs2(VitJob A, VitJob B, int nwa, int wa0) {
     __shared__ AcsLds<1> L;
     const int b = blockIdx.x;
-    if (b < nwa) acs_body<KA, 1, B8>(A, xcd_order(b, nwa), L);
+    if (b < nwa) acs_body<KA, 1, B8>(A, wa0 + xcd_order(b, nwa), L);
     else acs_body<KB, 1, B8>(B, xcd_order(b - nwa, gridDim.x - nwa), L);
 }
 // LDS (dynamic): the staging buffer, then tb_prbs_words(dec_nch) PRBS words
@@ -1010,9 +1011,9 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     tb_body<KIND>(J, blockIdx.x, tb_lds, tb_lds + TB_WORDS);
 }
 template <int KA, int KB>
-__global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba) {
+__global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba, int ba0) {
     extern __shared__ uint32_t tb_lds[];
-    if ((int)blockIdx.x < nba) tb_body<KA>(A, blockIdx.x, tb_lds, tb_lds + TB_WORDS);
+    if ((int)blockIdx.x < nba) tb_body<KA>(A, ba0 + blockIdx.x, tb_lds, tb_lds + TB_WORDS);
     else tb_body<KB>(B, blockIdx.x - nba, tb_lds, tb_lds + TB_WORDS);
 }
 static size_t tb_lds_bytes(int nch) { return 4 * (size_t)(TB_WORDS + tb_prbs_words(nch)); }
@@ -1088,23 +1089,36 @@ hipError_t launch_viterbi(hipStream_t st, const VitJob &job) {
     hipError_t e = launch_acs(st, job);
     return e != hipSuccess ? e : launch_traceback(st, job);
 }
-// MSC (a) and FIC (b) decoded by one ACS launch and one traceback launch
-hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+// MSC (a) and FIC (b) decoded by one ACS launch and one traceback launch.  The _range
+// forms decode the MSC's traceback blocks [b0, b1) (64 codewords each; the ACS's waves
+// 32 b0 .. 32 b1) and, with fic, the FIC: slices of the batch (DABGPU_VIT_SLICES A/B)
+hipError_t launch_acs_msc_fic_range(hipStream_t st, const VitJob &a, const VitJob &b, int b0, int b1, bool fic) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
     if (a.dec_ncw < dec_rows(a.n_cw) || b.dec_ncw < dec_rows(b.n_cw) || a.dec_nch <= 0 || b.dec_nch <= 0)
         return hipErrorInvalidValue;
     if (a.ring8 != b.ring8) return hipErrorInvalidValue;
-    const int nwa = (a.n_cw + 1) / 2, nwb = (b.n_cw + 1) / 2;
-    if (a.ring8) hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC, true>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
-    else hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa);
+    const int nwa_all = (a.n_cw + 1) / 2, nwb = fic ? (b.n_cw + 1) / 2 : 0;
+    const int w0 = b0 * (TB_CW / 2), w1 = min(nwa_all, b1 * (TB_CW / 2));
+    if (b0 < 0 || w0 >= w1) return hipErrorInvalidValue;
+    const int nwa = w1 - w0;
+    if (a.ring8) hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC, true>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa, w0);
+    else hipLaunchKernelGGL((k_acs2<SRC_MSC, SRC_FIC>), dim3(nwa + nwb), dim3(64), 0, st, a, b, nwa, w0);
     return hipGetLastError();
 }
-hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+hipError_t launch_traceback_msc_fic_range(hipStream_t st, const VitJob &a, const VitJob &b, int b0, int b1, bool fic) {
     if (a.kind != SRC_MSC || b.kind != SRC_FIC || a.n_cw <= 0 || b.n_cw <= 0) return hipErrorInvalidValue;
-    const int nba = (a.n_cw + TB_CW - 1) / TB_CW, nbb = (b.n_cw + TB_CW - 1) / TB_CW;
-    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(nba + nbb), dim3(64),
-                       tb_lds_bytes(max(a.dec_nch, b.dec_nch)), st, a, b, nba);
+    const int nba_all = (a.n_cw + TB_CW - 1) / TB_CW, nbb = fic ? (b.n_cw + TB_CW - 1) / TB_CW : 0;
+    b1 = min(b1, nba_all);
+    if (b0 < 0 || b0 >= b1) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(b1 - b0 + nbb), dim3(64),
+                       tb_lds_bytes(max(a.dec_nch, b.dec_nch)), st, a, b, b1 - b0, b0);
     return hipGetLastError();
+}
+hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+    return launch_acs_msc_fic_range(st, a, b, 0, (a.n_cw + TB_CW - 1) / TB_CW, true);
+}
+hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {
+    return launch_traceback_msc_fic_range(st, a, b, 0, (a.n_cw + TB_CW - 1) / TB_CW, true);
 }
 
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib, const uint8_t *tabs,
