@@ -101,7 +101,9 @@ def dist_setup(n_gpus):
         # (profiles/r05_rccl_overhead_ab.txt), so RCCL is used only where the data moves (the C4
         # leg's transfers, after the rank-local legs)
         global _CTL
-        _CTL = td.new_group(backend="gloo") if backend == "nccl" else None
+        # (DAB_CTL_RCCL=1, A/B only: the control collectives on the RCCL group, as round 5's
+        # first N > 1 path ran them -- tools/rccl_overhead.sh)
+        _CTL = td.new_group(backend="gloo") if backend == "nccl" and os.environ.get("DAB_CTL_RCCL") != "1" else None
         if backend == "nccl" and os.environ.get("DAB_RCCL_EARLY") == "1":
             # A/B hook (tools/rccl_overhead.sh): create the RCCL communicator before the
             # rank-local legs, as round 5's first N > 1 path did
@@ -138,7 +140,8 @@ def allreduce_max(dist, x):
     if dist is None:
         return x
     import torch
-    t = torch.tensor([x], dtype=torch.float64)       # on the host: the gloo control group
+    dev = "cuda" if _CTL is None and dist.get_backend() == "nccl" else "cpu"   # (DAB_CTL_RCCL A/B)
+    t = torch.tensor([x], dtype=torch.float64, device=dev)   # on the host: the gloo control group
     dist.all_reduce(t, op=dist.ReduceOp.MAX, group=_CTL)
     return float(t.item())
 
