@@ -522,6 +522,27 @@ class Context:
                 if b is not None:
                     b.free()
 
+    def ofdm_symbol(self, samples: np.ndarray, kind: int = 0, spectrum: Optional[np.ndarray] = None):
+        """dabgpu_ofdm_symbol (ofdmDecoder::processBlock_0 / processToken one symbol at a
+        time): kind 0 = FFT of T_u samples (complex64 [2048]) -> the spectrum in natural bin
+        order; kind 1 = a data symbol (T_s samples) against `spectrum` -> (ibits [3072],
+        the new spectrum)."""
+        x = np.ascontiguousarray(samples, dtype=np.complex64).view(np.float32)
+        ds, dsp = self.put(x), self.buf(8 * 2048)
+        db = self.buf(2 * SYMBITS) if kind else None
+        try:
+            if spectrum is not None:
+                dsp.upload(np.ascontiguousarray(spectrum, dtype=np.complex64).view(np.float32))
+            _chk(lib().dabgpu_ofdm_symbol(self.h, ds.ptr, kind, dsp.ptr, db.ptr if db else None), "ofdm_symbol")
+            sp = dsp.download(np.float32, (2048, 2))
+            self.check()
+            spec = sp[:, 0] + 1j * sp[:, 1]
+            return (db.download(np.int16, SYMBITS), spec) if kind else spec
+        finally:
+            for b in (ds, dsp, db):
+                if b is not None:
+                    b.free()
+
     def nco_eval(self, first: int = 0, n: int = 2048000) -> np.ndarray:
         """oscillatorTable[first:first+n] as the front-end kernels compute it
         (dabgpu_nco_eval): float32 [n, 2]"""

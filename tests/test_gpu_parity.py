@@ -501,6 +501,29 @@ def test_demod_fft_equals_restated_transform(ctx, fmt):
     print(f"{fmt}: {nsym} spectra of 2048 bins equal the restated transform bit for bit")
 
 
+def test_fft2048_wg_equals_restated_transform(ctx):
+    """fft2048_wg in its plain form -- pass 4 as DPP moves + fmas, the transform of findIndex
+    (phasereference.cpp:60-88), processBlock_0 (ofdm-decoder.cpp:85-162) and the one-symbol
+    drop-in -- bit for bit against tests/gpu_fft_emu.py, through dabgpu_ofdm_symbol (kind 0):
+    complex Gaussian vectors at several scales, a pure carrier, an impulse, zeros, and
+    mixed Mode-I symbols"""
+    import gpu_fft_emu
+    rng = np.random.default_rng(17)
+    xs = [(rng.normal(size=2048) + 1j * rng.normal(size=2048)) * s for s in (1.0, 1e-3, 37.0)]
+    xs.append(np.exp(2j * np.pi * 123.25 * np.arange(2048) / 2048))
+    xs.append(np.eye(1, 2048, 5)[0] * (0.5 + 0.25j))
+    xs.append(np.zeros(2048))
+    g, x, frs = _cfo_frames(1300.0)
+    for fr in frs[:2]:
+        xs.append(x[fr.block0:fr.block0 + 2048, 0] + 1j * x[fr.block0:fr.block0 + 2048, 1])
+    for i, v in enumerate(xs):
+        v = v.astype(np.complex64)
+        got = ctx.ofdm_symbol(v).astype(np.complex64)
+        want = gpu_fft_emu.gpu_fft(v[None, :])[0]
+        neq = (got.real != want.real) | (got.imag != want.imag)
+        assert not neq.any(), (i, int(neq.sum()), np.flatnonzero(neq)[:4].tolist())
+
+
 # ---------------------------------------------------------------- pipeline
 def _pipeline_decode(ctx, ens_list, F, subch, cfo=0.0, snr=300.0, runs=2):
     import dabamd
