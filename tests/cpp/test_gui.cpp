@@ -255,9 +255,14 @@ int main(int argc, char **argv) {
             n_spec++;
         };
         dabgpu::ofdmDecoder::iq_count = 0;          // a fresh GUI process: processToken's static cnt is 0
+        // the packet pass also feeds an IQ ring and sets an out-of-range display token (ADVICE r5:
+        // a token outside 1..75 turns the display feed off -- as in the reference, where it never
+        // matches blkno -- and the decode goes on)
+        dabgpu::RingBuffer<dabgpu::DSPCOMPLEX> iq2(2 * 1536);
         {
             dabgpu::ofdmProcessor ofdm(&input, &p, kind == 0 ? os : dabgpu::ofdmProcessor::signals{}, &msch, &fic, 3,
-                                       kind == 0 ? &spectrumBuffer : nullptr, kind == 0 ? &iqBuffer : nullptr, 1);
+                                       kind == 0 ? &spectrumBuffer : nullptr, kind == 0 ? &iqBuffer : &iq2, 1);
+            if (kind == 1) ofdm.set_displayToken(99);
             CHECK(wait_for([&] { return ofdm.frames() >= NF; }, 60), "part B frames %lld", (long long)ofdm.frames());
             std::this_thread::sleep_for(std::chrono::milliseconds(100));
             frames = ofdm.frames();
