@@ -989,171 +989,6 @@ __device__ __forceinline__ void tb_body(const VitJob &J, int blk, uint32_t *stag
     }
 }
 
-// Lean traceback (A/B, -DTB_LITE=1): the same chainback and output as tb_body, with a small
-// footprint so the next run's demod keeps its occupancy beside it (the ring form holds 340
-// VGPRs + 17 KB of LDS per wave: a SIMD with one traceback wave has room for one demod wave).
-// Two waves per 64 codewords: wave 0 walks, reading each step pair's three decision words
-// straight from the cache hierarchy (row = its codeword, 64 words per chunk); wave 1 stays
-// at most TB_LITE_AHEAD chunks ahead of it and touches every 128-B line of the next chunks,
-// so the walker's loads hit L2 instead of HBM -- the prefetcher waits for its own loads,
-// the walker never does (vmcnt is per wave).  LDS: the PRBS words and a progress word.
-#ifndef TB_LITE_AHEAD
-#define TB_LITE_AHEAD 2
-#endif
-template <int KIND>
-__device__ __forceinline__ void tb_body_lite(const VitJob &J, int blk, uint32_t *prbs_l, volatile int32_t *prog) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int cw = blk * TB_CW + lane;
-    bool act = cw < J.n_cw;
-    int N = 0, prof = 0;
-    if (act) {
-        if constexpr (KIND == SRC_MSC) {
-            const int sub = cw % J.nsub;
-            const int cl = (cw / J.nsub) % J.ncif;
-            const int stream = cw / J.nsub / J.ncif;
-            prof = sub;
-            act = cl < J.ncifs[stream] && J.cif0s[stream] + cl >= 16;
-        } else if constexpr (KIND == SRC_FRAG) {
-            prof = J.cw_prof ? J.cw_prof[cw] : 0;
-        } else if constexpr (KIND == SRC_FIC) {
-            act = J.slots[cw >> 2] >= 0;
-        }
-        if (J.valid && !J.valid[cw]) act = false;
-        if (act) N = J.prof[prof].nbits;
-    }
-    int tmax = act ? N + 6 : 0;
-    for (int o = 32; o > 0; o >>= 1) tmax = max(tmax, __shfl_xor(tmax, o));
-    tmax = __builtin_amdgcn_readfirstlane(tmax);
-    if (tmax == 0) return;                               // both waves: the same codewords
-    const int nch = (tmax + WS - 1) / WS;
-    const uint32_t *blk0 = J.dec + dec_word_index((int64_t)blk * TB_CW, J.dec_nch);
-    const __amdgpu_buffer_rsrc_t drs = __builtin_amdgcn_make_buffer_rsrc((void *)blk0, (short)0, -1, 0x00020000);
-    if (wave == 1) {
-        // the prefetcher: chunk ch's 16 KB is 128 lines of 128 B; lane l touches lines l and
-        // l + 64, and waits for them (its own vmcnt) before the next chunk
-        uint32_t sink = 0;
-        for (int ch = nch - 1; ch >= 0; ch--) {
-            while (*prog > ch + TB_LITE_AHEAD) __builtin_amdgcn_s_sleep(2);
-            const int o = ch * 4096 * 4 + lane * 128;
-            sink ^= __builtin_amdgcn_raw_buffer_load_b32(drs, o, 0, 0) ^
-                    __builtin_amdgcn_raw_buffer_load_b32(drs, o + 64 * 128, 0, 0);
-        }
-        if (sink == 0x9E3779B9u) prog[1] = (int32_t)sink;   // keeps the loads (a spare LDS word)
-        return;
-    }
-    const int steps = act ? N + 6 : 0;
-    int smin = act ? steps : tmax;
-    for (int o = 32; o > 0; o >>= 1) smin = min(smin, __shfl_xor(smin, o));
-    smin = __builtin_amdgcn_readfirstlane(smin);
-    uint8_t *out = J.out + (act ? (int64_t)cw * J.out_stride : 0);
-    if (J.prbs) {
-        const int nw = tb_prbs_words(nch);
-        for (int i = lane; i < nw; i += 64) prbs_l[i] = J.prbs_words[i];
-        wave_sync();
-    }
-    int lr = 0;
-    uint32_t gb[TB_GROUP];
-#pragma unroll
-    for (int i = 0; i < TB_GROUP; i++) gb[i] = 0;
-    const bool al16 = (((uintptr_t)J.out | (uintptr_t)J.out_stride) & 15) == 0;
-    const bool al2 = (((uintptr_t)J.out | (uintptr_t)J.out_stride) & 1) == 0;
-    auto pk16 = [](uint32_t x) {
-        const uint32_t r = __builtin_bitreverse32(x) >> 16;
-        return (r >> 8) | ((r & 0xFFu) << 8);
-    };
-    auto flush = [&](int g) {                             // as tb_body's
-        const int tg = WS * TB_GROUP * g;
-        if (!act || tg >= N) return;
-        if (J.packed) {
-            uint8_t *ob = out + tg / 8;
-            if (al2 && tg + WS * TB_GROUP <= N) {
-#pragma unroll
-                for (int q = 0; q < WS * TB_GROUP / 16; q++) {
-                    const int b = 16 * q, c = b / WS, r = b % WS;
-                    uint32_t x = gb[c] >> r;
-                    if (r > WS - 16) x |= gb[c + 1] << (WS - r);
-                    *(uint16_t *)(ob + 2 * q) = (uint16_t)pk16(x & 0xFFFFu);
-                }
-            } else {
-                const int nb = min(WS * TB_GROUP, N - tg) / 8;
-#pragma unroll
-                for (int q = 0; q < WS * TB_GROUP / 8; q++) {
-                    const int b = 8 * q, c = b / WS, r = b % WS;
-                    if (q < nb) {
-                        uint32_t x = gb[c] >> r;
-                        if (r > WS - 8) x |= gb[c + 1] << (WS - r);
-                        ob[q] = (uint8_t)(__builtin_bitreverse32(x & 0xFFu) >> 24);
-                    }
-                }
-            }
-            return;
-        }
-        if (al16 && tg + WS * TB_GROUP <= N) {
-#pragma unroll
-            for (int q = 0; q < WS * TB_GROUP / 16; q++) {
-                uint32_t d[4];
-#pragma unroll
-                for (int e = 0; e < 4; e++) {
-                    const int b = 16 * q + 4 * e, c = b / WS, r = b % WS;
-                    uint32_t x = gb[c] >> r;
-                    if (r > WS - 4) x |= gb[c + 1] << (WS - r);
-                    d[e] = ((x & 0xFu) * 0x204081u) & 0x01010101u;
-                }
-                *(uint4 *)(out + tg + 16 * q) = make_uint4(d[0], d[1], d[2], d[3]);
-            }
-        } else {
-#pragma unroll
-            for (int k = 0; k < TB_GROUP; k++) {
-                const int base = tg + WS * k, nk = min(WS, N - base);
-                for (int i = 0; i < nk; i++) out[base + i] = (uint8_t)((gb[k] >> i) & 1u);
-            }
-        }
-    };
-    for (int ch = nch - 1; ch >= 0; ch--) {
-        if (lane == 0) *prog = ch;                       // the prefetcher's pace
-        // this lane's row of chunk ch: word j at byte offset 4 (4096 ch + 64 lane + j)
-        const int rowb = (ch * 4096 + lane * 64) * 4;
-        auto word = [&](int j) { return __builtin_amdgcn_raw_buffer_load_b32(drs, rowb + 4 * j, 0, 0); };
-        const int t0 = ch * WS;
-        uint32_t w = 0;
-        const bool full = t0 + WS <= steps;
-#pragma unroll
-        for (int k = WS - 1; k >= 1; k -= 2) {
-            const int p1 = 5 - (k % 6), p2 = 5 - ((k - 1) % 6);
-            const uint32_t w1 = word(lr), c0 = word(lr & ~(1 << p1)), c1 = word(lr | (1 << p1));
-            {
-                const int d = (int)((w1 >> dpos(k)) & 1u);
-                const int u = (lr >> p1) & 1;
-                const int nl = (lr & ~(1 << p1)) | (d << p1);
-                if (t0 + WS <= smin || full || t0 + k < steps) {
-                    lr = nl;
-                    w |= (uint32_t)u << k;
-                }
-            }
-            {
-                const uint32_t w2 = ((lr >> p1) & 1) ? c1 : c0;
-                const int d = (int)((w2 >> dpos(k - 1)) & 1u);
-                const int u = (lr >> p2) & 1;
-                const int nl = (lr & ~(1 << p2)) | (d << p2);
-                if (t0 + WS <= smin || full || t0 + k - 1 < steps) {
-                    lr = nl;
-                    w |= (uint32_t)u << (k - 1);
-                }
-            }
-        }
-        if (J.prbs) {
-            const int wi = t0 >> 5, sh = t0 & 31;
-            const uint32_t lo = prbs_l[wi], hi = prbs_l[wi + 1];
-            w ^= (sh ? (lo >> sh) | (hi << (32 - sh)) : lo) & 0x3FFFFFFFu;
-        }
-#pragma unroll
-        for (int i = TB_GROUP - 1; i > 0; i--) gb[i] = gb[i - 1];
-        gb[0] = w;
-        if (ch % TB_GROUP == 0) flush(ch / TB_GROUP);
-    }
-    if (lane == 0) *prog = -TB_LITE_AHEAD - 1;           // (the prefetcher has left by now)
-}
-
 template <int KIND, bool B8 = false>
 __global__ __launch_bounds__(64, 8) void k_acs(VitJob J) {
     __shared__ AcsLds<1> L;
@@ -1175,29 +1010,12 @@ __global__ __launch_bounds__(64) void k_traceback(VitJob J) {
     extern __shared__ uint32_t tb_lds[];
     tb_body<KIND>(J, blockIdx.x, tb_lds, tb_lds + TB_WORDS);
 }
-#ifndef TB_LITE
-#define TB_LITE 0
-#endif
-#if TB_LITE
-constexpr int TB_THREADS = 128;
-template <int KA, int KB>
-__global__ __launch_bounds__(128) void k_traceback2(VitJob A, VitJob B, int nba, int ba0) {
-    extern __shared__ uint32_t tb_lds[];
-    volatile int32_t *prog = (volatile int32_t *)tb_lds;
-    if (threadIdx.x == 0) prog[0] = 1 << 30;
-    __syncthreads();
-    if ((int)blockIdx.x < nba) tb_body_lite<KA>(A, ba0 + blockIdx.x, tb_lds + 4, prog);
-    else tb_body_lite<KB>(B, blockIdx.x - nba, tb_lds + 4, prog);
-}
-#else
-constexpr int TB_THREADS = 64;
 template <int KA, int KB>
 __global__ __launch_bounds__(64) void k_traceback2(VitJob A, VitJob B, int nba, int ba0) {
     extern __shared__ uint32_t tb_lds[];
     if ((int)blockIdx.x < nba) tb_body<KA>(A, ba0 + blockIdx.x, tb_lds, tb_lds + TB_WORDS);
     else tb_body<KB>(B, blockIdx.x - nba, tb_lds, tb_lds + TB_WORDS);
 }
-#endif
 static size_t tb_lds_bytes(int nch) { return 4 * (size_t)(TB_WORDS + tb_prbs_words(nch)); }
 
 // FIB CRC check (dab-constants.h:310-340): invert the 16 CRC bits in place, run
@@ -1292,8 +1110,8 @@ hipError_t launch_traceback_msc_fic_range(hipStream_t st, const VitJob &a, const
     const int nba_all = (a.n_cw + TB_CW - 1) / TB_CW, nbb = fic ? (b.n_cw + TB_CW - 1) / TB_CW : 0;
     b1 = min(b1, nba_all);
     if (b0 < 0 || b0 >= b1) return hipErrorInvalidValue;
-    const size_t lds = TB_LITE ? 4 * (4 + (size_t)tb_prbs_words(max(a.dec_nch, b.dec_nch))) : tb_lds_bytes(max(a.dec_nch, b.dec_nch));
-    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(b1 - b0 + nbb), dim3(TB_THREADS), lds, st, a, b, b1 - b0, b0);
+    hipLaunchKernelGGL((k_traceback2<SRC_MSC, SRC_FIC>), dim3(b1 - b0 + nbb), dim3(64),
+                       tb_lds_bytes(max(a.dec_nch, b.dec_nch)), st, a, b, b1 - b0, b0);
     return hipGetLastError();
 }
 hipError_t launch_acs_msc_fic(hipStream_t st, const VitJob &a, const VitJob &b) {

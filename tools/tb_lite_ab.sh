@@ -1,6 +1,8 @@
 #!/bin/bash
 # The lean traceback (TB_LITE) against the product's: parity of the variant on the pipeline
 # tests, then interleaved bench runs.   tools/tb_lite_ab.sh OUT REPS
+# (the variant: git apply tools/tb_lite.patch && tools/build_variant.sh r06tblite -DTB_LITE=1;
+#  the base: lib/variants/libdabgpu_r06main.so, a copy of the product's library)
 set -o pipefail
 O=$1; REPS=${2:-3}
 V=$PWD/sdr-j-dab_amd/lib/variants
