@@ -537,6 +537,8 @@ def main():
     ap.add_argument("--solo-steps", type=int, default=2,
                     help="steps after the timed region with every kernel alone on the device (profiling mode 3): "
                          "per-kernel times without overlap, to name the dominant kernel")
+    ap.add_argument("--delivered-fic", choices=["bytes", "bits"], default="bytes",
+                    help="FIC format of the delivered leg: FIB bytes (DABGPU_PACK_FIC) or one bit per byte")
     ap.add_argument("--delivered-steps", type=int, default=10,
                     help="timed steps after the main measurement whose FIC bits + CRCs and MSC bytes (8 bits per "
                          "byte) are copied to pinned host memory while the next step decodes (dabgpu_pipe_fetch): "
@@ -669,7 +671,8 @@ def main():
     delivered = None
     if deliv_steps:
         k0 = ck + 1 + args.solo_steps
-        delivered = delivered_leg(dabamd, ctx, pipe, step, k0, deliv_steps - 1, E, F, SUBCH, dabplus, dist, truth, P)
+        delivered = delivered_leg(dabamd, ctx, pipe, step, k0, deliv_steps - 1, E, F, SUBCH, dabplus, dist, truth, P,
+                                  fic_bytes=args.delivered_fic == "bytes")
     sync_loss = None
     if loss_steps and E >= 2:
         k0 = ck + 1 + args.solo_steps + deliv_steps
@@ -996,15 +999,17 @@ def c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus
                     "kernels' loads).  Link-bound by design: DESIGN.md section 7"}
 
 
-def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist, truth, P):
+def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist, truth, P, fic_bytes=True):
     """`steps` timed steps whose outputs are copied to pinned host memory (two sets,
     alternating like the pipeline's device outputs), each copy on its run's back-end
     stream behind the channel decoding (dabgpu_pipe_fetch), overlapping the next run.
     The last step's host copy of ensemble 0 is checked against the transmitted bits."""
     pipe.sync()
-    pipe.set_packed(True)
+    msc_packed = pipe.packed
+    pipe.set_packed(dabamd.PACK_MSC | (dabamd.PACK_FIC if fic_bytes else 0))    # MSC bytes, FIBs as bytes
     ns = len(subch)
-    n_fic, n_crc = E * F * 4 * 768, E * F * 12
+    fb = 96 if fic_bytes else 768                               # bytes per FIC block
+    n_fic, n_crc = E * F * 4 * fb, E * F * 12
     n_msc = E * 4 * F * ns * pipe.msc_stride_packed
     nd = len(pipe.dp)
     if nd:                                                      # only the run's superframes travel
@@ -1039,21 +1044,25 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
     barrier(dist)
     st1 = pipe.state(0)
     h = hb[steps & 1]
-    fic = h.view(np.uint8, (E, F, 4, 768))
+    fic = h.view(np.uint8, (E, F, 4, fb))
+    if fic_bytes:
+        fic = np.unpackbits(fic, axis=-1)
     crc = h.view(np.uint8, (E, F, 12), n_fic)
     msc = np.unpackbits(h.view(np.uint8, (E, 4 * F, ns, pipe.msc_stride_packed), n_fic + n_crc), axis=-1)
     check = check_step(truth, P, st0, st1, fic, crc, msc, valids[steps & 1], subch)
     for b in hb:
         b.free()
+    pipe.sync()
+    pipe.set_packed(dabamd.PACK_MSC if msc_packed else 0)      # the timed legs' format again
     if nd:
-        pipe.sync()
         pipe.set_dabplus_compact(False)
     world = dist.get_world_size() if dist is not None else 1
     return {"value": world * E * F * 76 * steps / el, "ms_per_step": el / steps * 1e3, "steps": steps,
             "bytes_to_host_per_step": total, "pcie_GBps": total * steps / el / 1e9,
             "msc_format": "8 bits per byte, msb first (dabgpu_pipe_set_packed)",
+            "fic_format": "FIB bytes, 96 per FIC block (DABGPU_PACK_FIC)" if fic_bytes else "1 bit per byte",
             "checked_last_step_from_host_memory": check,
-            "note": "FIC bits + CRC flags + packed MSC bytes" + (" + DAB+ superframe records and the run's "
+            "note": "FIC + CRC flags + packed MSC bytes" + (" + DAB+ superframe records and the run's "
                                                                  "superframe bytes (compact)" if nd else "")
                     + " of every step copied to pinned host memory behind its run's channel decoding "
                       "(dabgpu_pipe_fetch), overlapping the next run"}

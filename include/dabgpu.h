@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DABGPU_ABI_VERSION 6
+#define DABGPU_ABI_VERSION 7
 
 /* error codes */
 #define DABGPU_OK          0
@@ -447,10 +447,20 @@ int dabgpu_pipe_set_display(dabgpu_pipe *p, int on);
 /* The symbol (1..75) the display feed keeps, ofdmDecoder::set_displayToken (declared in
  * ofdm-decoder.h:50, displayToken = 2 at ofdm-decoder.cpp:61); takes effect at the next run. */
 int dabgpu_pipe_set_display_token(dabgpu_pipe *p, int token);
-/* MSC output format of the following runs: on = 0 (default) one bit per byte, as
- * deconvolve delivers it (viterbi.cpp:240-241); on = 1 eight bits per byte, msb first
- * (the packing of mp4Processor::addtoFrame, mp4processor.cpp:115-121 -- numpy packbits
- * order): msc_stride is then in bytes (>= 3 * bitRate).  The DAB+ layer reads either. */
+/* Output format of the following runs, a mask (0 = the default: one bit per byte, as
+ * deconvolve / process_ficInput deliver them, viterbi.cpp:240-241, fic-handler.cpp:270-292):
+ *   DABGPU_PACK_MSC  MSC eight bits per byte, msb first (the packing of
+ *                    mp4Processor::addtoFrame, mp4processor.cpp:115-121 -- numpy packbits
+ *                    order): msc_stride is then in bytes (>= 3 * bitRate).  The DAB+ layer
+ *                    reads either.
+ *   DABGPU_PACK_FIC  FIC as FIB bytes, msb first: fic_bits holds [n_frames][4][96] bytes per
+ *                    stream (3 FIBs of 32 bytes per FIC block, the last 2 bytes of each FIB
+ *                    its CRC, inverted in place as check_CRC_bits leaves it,
+ *                    dab-constants.h:310-340) instead of [4][768] bits -- an eighth of the
+ *                    bytes a host (or dabgpu_pipe_fetch) has to move; fic_crc unchanged.
+ * Any other value: DABGPU_E_ARG. */
+#define DABGPU_PACK_MSC 1
+#define DABGPU_PACK_FIC 2
 int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on);
 /* Copy bytes from an output buffer of the last dabgpu_pipe_run (or dabgpu_pipe_dabplus)
  * to host memory, asynchronously, behind that run's channel decoding on its back-end

@@ -207,7 +207,7 @@ hipError_t launch_acs_msc_fic_range(hipStream_t st, const VitJob &msc, const Vit
 hipError_t launch_traceback_msc_fic_range(hipStream_t st, const VitJob &msc, const VitJob &fic, int b0, int b1,
                                           bool with_fic);
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *crc_ok, int n_fib, const uint8_t *tabs,
-                           const int32_t *slots = nullptr);
+                           const int32_t *slots = nullptr, bool packed = false);
 hipError_t launch_dabplus(hipStream_t st, const DpJob &job);
 hipError_t launch_iq_convert(hipStream_t st, int format, const void *src, int64_t n_values, float *dst);
 // device -> mapped pinned host memory by `wgs` workgroups; src, dst, bytes 16-byte aligned

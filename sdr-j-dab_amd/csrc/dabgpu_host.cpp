@@ -944,6 +944,7 @@ struct dabgpu_pipe {
     float2 *disp_d = nullptr;        // [S][R][K]
     bool display = false;
     bool packed = false;             // MSC output 8 bits per byte (dabgpu_pipe_set_packed)
+    bool fic_packed = false;         // FIC output as FIB bytes (DABGPU_PACK_FIC)
     int iq_fmt = DABGPU_IQ_F32;      // sample format of the streams (dabgpu_pipe_set_iq_format)
     int disp_token = 2;              // the display feed's symbol (ofdm-decoder.cpp:61 displayToken)
     // background null search (DABGPU_CTL_ACQ_ASYNC, the default since round 6): a stream
@@ -1691,7 +1692,8 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
             JF.prof = (const Profile *)p->ficprof_d;
             JF.inv = c->fic_inv;
             JF.out = fic_bits;
-            JF.out_stride = 768;
+            JF.out_stride = p->fic_packed ? 96 : 768;     // 3 FIBs of 32 bytes, or 768 bits
+            JF.packed = p->fic_packed ? 1 : 0;
             JF.prbs = 1;
             JF.prbs_words = c->prbs;
             JF.dec = p->dec_d[par] + p->dec_fic_off;
@@ -1753,7 +1755,7 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
             HIPCHK(hipEventRecord(p->ev_tb, p->ts));
             HIPCHK(hipStreamWaitEvent(bs, p->ev_tb, 0));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d, p->fic_packed));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         } else if (fic_bits && do_msc) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
@@ -1765,14 +1767,14 @@ int dabgpu_pipe_run(dabgpu_pipe *p, const void *iq, int64_t stride, const int64_
             HIPCHK(launch_traceback_msc_fic(bs, JM, JF));
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_TB, false));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
-            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d, p->fic_packed));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         } else if (fic_bits) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, true));
             HIPCHK(launch_viterbi(bs, JF));
             HIPCHK(hipEventRecord(p->ev_acs[par], bs));
             p->acs_rec[par] = true;
-            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d));
+            if (fic_crc) HIPCHK(launch_fic_post(bs, fic_bits, fic_crc, 12 * S * F, c->dptab, slots_d, p->fic_packed));
             HIPCHK(prof_mark(p, DABGPU_STAGE_FIC, false));
         } else if (do_msc) {
             HIPCHK(prof_mark(p, DABGPU_STAGE_MSC_ACS, true));
@@ -2085,8 +2087,9 @@ int dabgpu_pipe_frame_slot(dabgpu_pipe *p, int frame, int32_t *slot) {
     return 0;
 }
 int dabgpu_pipe_set_packed(dabgpu_pipe *p, int on) {
-    if (!p) return fail(DABGPU_E_ARG, "bad args");
-    p->packed = on != 0;
+    if (!p || on < 0 || on > (DABGPU_PACK_MSC | DABGPU_PACK_FIC)) return fail(DABGPU_E_ARG, "packing %d", on);
+    p->packed = (on & DABGPU_PACK_MSC) != 0;
+    p->fic_packed = (on & DABGPU_PACK_FIC) != 0;
     return 0;
 }
 int dabgpu_pipe_set_iq_format(dabgpu_pipe *p, int format) {

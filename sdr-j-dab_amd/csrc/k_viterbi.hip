@@ -1025,9 +1025,12 @@ static size_t tb_lds_bytes(int nch) { return 4 * (size_t)(TB_WORDS + tb_prbs_wor
 // No LDS allocation: the kernel runs beside the next run's demod, whose workgroups hold
 // all of a CU's LDS (the 512-byte table is read through the caches instead).
 // slots (optional): ring slot per frame (12 FIBs), < 0 = frame not committed: no check, ok = 0
+// packed: the FIBs as 32 bytes each, msb first (dabgpu_pipe_set_packed DABGPU_PACK_FIC): lane l
+// takes the nibble of bits 4l..4l+3 (the high nibble of byte l/2 for even l), the CRC bytes
+// 30 and 31 are inverted by their even lanes
 __global__ __launch_bounds__(256) void k_fic_post(uint8_t *__restrict__ bits, uint8_t *__restrict__ ok, int n_fib,
                                                   const int32_t *__restrict__ slots,
-                                                  const uint16_t *__restrict__ tab) {
+                                                  const uint16_t *__restrict__ tab, int packed) {
     const int lane = threadIdx.x & 63;
     const int f = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (f >= n_fib) return;
@@ -1035,11 +1038,23 @@ __global__ __launch_bounds__(256) void k_fic_post(uint8_t *__restrict__ bits, ui
         if (lane == 0) ok[f] = 0;
         return;
     }
-    uint32_t *w = (uint32_t *)(bits + (int64_t)f * 256) + lane;
-    uint32_t v = *w;
-    if (lane >= 60) {                                    // bits 240..255: the CRC, inverted
-        v ^= 0x01010101u;
-        *w = v;
+    uint32_t v;                                          // bit 4l + e of the FIB at bit 8e
+    if (packed) {
+        uint8_t *b = bits + (int64_t)f * 32 + (lane >> 1);
+        uint32_t x = *b;
+        if (lane >= 60) {                                // bytes 30, 31: the CRC, inverted
+            x ^= 0xFFu;
+            if (!(lane & 1)) *b = (uint8_t)x;
+        }
+        const uint32_t nib = (lane & 1) ? x & 0xFu : x >> 4;    // bit 4l + e at bit 3 - e
+        v = ((nib >> 3) & 1u) | (((nib >> 2) & 1u) << 8) | (((nib >> 1) & 1u) << 16) | ((nib & 1u) << 24);
+    } else {
+        uint32_t *w = (uint32_t *)(bits + (int64_t)f * 256) + lane;
+        v = *w;
+        if (lane >= 60) {                                // bits 240..255: the CRC, inverted
+            v ^= 0x01010101u;
+            *w = v;
+        }
     }
     uint32_t r = 0;
 #pragma unroll
@@ -1122,10 +1137,10 @@ hipError_t launch_traceback_msc_fic(hipStream_t st, const VitJob &a, const VitJo
 }
 
 hipError_t launch_fic_post(hipStream_t st, uint8_t *bits, uint8_t *ok, int n_fib, const uint8_t *tabs,
-                           const int32_t *slots) {
+                           const int32_t *slots, bool packed) {
     if (n_fib <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_fic_post, dim3((n_fib + 3) / 4), dim3(256), 0, st, bits, ok, n_fib, slots,
-                       (const uint16_t *)(tabs + FIBCRC_OFF));
+                       (const uint16_t *)(tabs + FIBCRC_OFF), packed ? 1 : 0);
     return hipGetLastError();
 }
 

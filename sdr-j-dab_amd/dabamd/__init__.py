@@ -73,6 +73,7 @@ class FrameInfo(C.Structure):
 
 CTL_RESET, CTL_COARSE_ON, CTL_COARSE_OFF, CTL_SCAN_ON, CTL_SCAN_OFF, CTL_RESYNC = 1, 2, 3, 4, 5, 6
 CTL_ACQ_ASYNC, CTL_ACQ_SYNC, CTL_INJECT_BOUNDS = 7, 8, 9
+PACK_MSC, PACK_FIC = 1, 2          # dabgpu_pipe_set_packed mask
 
 
 _lib: Optional[C.CDLL] = None
@@ -600,6 +601,7 @@ class Pipeline:
         self.msc_stride = (self.msc_stride + 15) // 16 * 16
         self.msc_stride_packed = self.msc_stride // 8        # bytes per codeword with set_packed
         self.packed = False
+        self.fic_packed = False
         self.iq_format = IQ_F32                              # dabgpu_pipe_set_iq_format's default
         # consecutive runs decode concurrently on two back-end streams (dabgpu.h,
         # dabgpu_pipe_sync): outputs alternate between two buffer sets
@@ -637,7 +639,7 @@ class Pipeline:
         if not download:
             return valid
         self.sync()
-        fic = self.fic_d.download(np.uint8, (self.S, self.F, 4, 768))
+        fic = self.fic_d.download(np.uint8, (self.S, self.F, 4, 96 if self.fic_packed else 768))
         crc = self.crc_d.download(np.uint8, (self.S, self.F, 12))
         msc = self.msc_d.download(np.uint8, (self.S, 4 * self.F, len(self.subch), ms)) if self.subch else None
         return fic, crc, msc, valid
@@ -715,12 +717,15 @@ class Pipeline:
         _chk(lib().dabgpu_pipe_frames(self.h, C.cast(fr, C.c_void_p), _p(si)), "dabgpu_pipe_frames")
         return list(fr), si.reshape(self.S, self.F)
 
-    def set_packed(self, on: bool = True) -> None:
-        """MSC output of the following runs: 8 bits per byte, msb first (packbits order)
-        instead of one bit per byte (dabgpu_pipe_set_packed); run() then returns
-        msc [S, 4F, n_subch, msc_stride_packed] bytes"""
-        _chk(lib().dabgpu_pipe_set_packed(self.h, int(on)), "dabgpu_pipe_set_packed")
-        self.packed = bool(on)
+    def set_packed(self, on=True) -> None:
+        """output format of the following runs (dabgpu_pipe_set_packed): True / PACK_MSC:
+        MSC 8 bits per byte, msb first (packbits order) instead of one bit per byte -- run()
+        then returns msc [S, 4F, n_subch, msc_stride_packed] bytes; | PACK_FIC: the FIC as
+        FIB bytes, fic [S, F, 4, 96]"""
+        m = PACK_MSC if on is True else 0 if on is False else int(on)
+        _chk(lib().dabgpu_pipe_set_packed(self.h, m), "dabgpu_pipe_set_packed")
+        self.packed = bool(m & PACK_MSC)
+        self.fic_packed = bool(m & PACK_FIC)
 
     def acquire_wait(self) -> None:
         """wait for a background null search in flight and apply it (dabgpu_pipe_acquire_wait)"""

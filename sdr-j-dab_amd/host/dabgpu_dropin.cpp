@@ -250,16 +250,17 @@ ensembleDecoder::ensembleDecoder(const config &cfg) : cfg_(cfg) {
         }
     }
     ndp_ = (int)dp_index_.size();
-    // the MSC leaves the GPU packed (8 bits per byte, 1/8 of the bytes over PCIe) and is
-    // unpacked here for the one-bit-per-byte consumers (dab-concurrent.cpp:191)
-    chk(dabgpu_pipe_set_packed(pipe_, 1), "dabgpu_pipe_set_packed");
+    // the MSC and the FIBs leave the GPU packed (8 bits per byte, 1/8 of the bytes over
+    // PCIe) and are unpacked here for the one-bit-per-byte consumers (dab-concurrent.cpp:191,
+    // fibProcessor::process_FIB)
+    chk(dabgpu_pipe_set_packed(pipe_, DABGPU_PACK_MSC | DABGPU_PACK_FIC), "dabgpu_pipe_set_packed");
     msc_stride_ = ((maxbits + 7) / 8 + 15) / 16 * 16;
     maxbits_ = maxbits;
     sf_stride_ = std::max(16, 110 * maxrs);
     const size_t SF = (size_t)cfg.n_streams * cfg.n_frames;
     // only the superframes a run completes cross PCIe (DABGPU_SF_SLOTS per subchannel)
     if (ndp_) chk(dabgpu_pipe_set_dabplus_compact(pipe_, 1), "dabgpu_pipe_set_dabplus_compact");
-    fic_.resize(SF * 4 * 768);
+    fic_.resize(SF * 4 * 96);
     crc_.resize(SF * 12);
     msc_.resize(std::max<size_t>(1, SF * 4 * cfg.subch.size() * msc_stride_));
     if (ndp_) {
@@ -415,16 +416,18 @@ bool ensembleDecoder::step() {
     // one that ran out of samples committed fewer): FIC and MSC for those
     std::vector<dabgpu_frame_info> fr((size_t)S * F);
     chk(dabgpu_pipe_frame_info(pipe_, fr.data()), "dabgpu_pipe_frame_info");
-    std::vector<uint8_t> fic((size_t)S * F * 4 * 768), crc((size_t)S * F * 12);
+    std::vector<uint8_t> fic((size_t)S * F * 4 * 96), crc((size_t)S * F * 12);
     fic_.download(fic.data(), fic.size());
     crc_.download(crc.data(), crc.size());
+    uint8_t fib[256];
     for (int s = 0; s < S && fib_cb_; s++)
         for (int f = 0; f < F; f++) {
             if (!fr[(size_t)s * F + f].committed) continue;
             for (int b = 0; b < 4; b++)
                 for (int k = 0; k < 3; k++) {
-                    const size_t o = (((size_t)s * F + f) * 4 + b) * 768 + 256 * k;
-                    fib_cb_(s, frames_done_[s] + f, b, fic.data() + o, crc[((size_t)s * F + f) * 12 + 3 * b + k] != 0);
+                    const uint8_t *pk = fic.data() + (((size_t)s * F + f) * 4 + b) * 96 + 32 * k;   // FIB bytes
+                    for (int i = 0; i < 256; i++) fib[i] = (uint8_t)((pk[i >> 3] >> (7 - (i & 7))) & 1);
+                    fib_cb_(s, frames_done_[s] + f, b, fib, crc[((size_t)s * F + f) * 12 + 3 * b + k] != 0);
                 }
         }
     if (NS && msc_cb_) {

@@ -74,8 +74,9 @@ def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=()
     pipe = dabamd.Pipeline(ctx, S, F, subs, freq_sync_method=method)
     if iq_format != IQ_F32:
         pipe.set_iq_format(iq_format)
-    if packed:                  # MSC bits 8 per byte (dabgpu_pipe_set_packed), unpacked here
-        pipe.set_packed(True)
+    if packed:                  # MSC bits 8 per byte (dabgpu_pipe_set_packed), unpacked here;
+        # packed == "fic": the FIC as FIB bytes too (DABGPU_PACK_FIC)
+        pipe.set_packed(dabamd.PACK_MSC | (dabamd.PACK_FIC if packed == "fic" else 0))
         pipe.msc_stride_packed += packed_pad    # a row stride that is not a multiple of 4 bytes
     if acq == "async":          # null searches in the background (DABGPU_CTL_ACQ_ASYNC) after the first
         pipe.acquire(diq, stride, [0] * S, lens)
@@ -96,6 +97,8 @@ def gpu_decode(ctx, iqs, F, runs, subch, method=1, n_avail=None, soft_streams=()
             fic, crc, msc, valid = pipe.run(diq, stride, na, partial=True)
             if packed and msc is not None:
                 msc = np.unpackbits(msc, axis=-1)
+            if packed == "fic":
+                fic = np.unpackbits(fic, axis=-1)
             dp = pipe.dabplus() if dpi else None
             fi = pipe.frame_info()
             frames, _ = pipe.frames()

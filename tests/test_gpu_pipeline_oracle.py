@@ -366,15 +366,17 @@ def test_c5_full_size_superframes_match_reference_path(ctx, fmt):
     assert bad == 0 and ok3 > 0
 
 
-@pytest.mark.parametrize("pad,fmt", [(0, F32), (1, F32), (0, S16), (0, U8)])
-def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad, fmt):
+@pytest.mark.parametrize("pad,fmt,packed", [(0, F32, True), (1, F32, True), (0, S16, True), (0, U8, True),
+                                            (0, S16, "fic"), (1, U8, "fic")])
+def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad, fmt, packed):
     """dabgpu_pipe_set_packed: the traceback writes the MSC bits 8 per byte (msb first,
     mp4processor.cpp:115-121's packing) and the DAB+ layer reads those bytes -- FIC, MSC
     and every superframe record equal the reference path, with UEP/EEP and DAB+
     subchannels side by side, near the decoding threshold.  pad 1: an odd row stride (the
     traceback's byte stores instead of 16-bit ones, the DAB+ layer's byte-wise window
-    copy instead of 4-byte loads)"""
-    packed = True
+    copy instead of 4-byte loads).  "fic": DABGPU_PACK_FIC as well -- the FIBs as bytes
+    (CRC bytes inverted in place, as check_CRC_bits leaves the bits) and the CRC flags of
+    the packed-byte check, both equal the reference path's"""
     sub = [(0, 96, 128, 3, 1, 0), (96, 48, 64, 0o103, 0, 1), (144, 24, 32, 0o104, 0, 0), (168, 36, 48, 0o103, 0, 1),
            (768, 96, 128, 3, 1, 0)]
     F, runs = 4, 5

@@ -248,7 +248,7 @@ def test_abi_library_exports_every_declared_symbol():
     lib = dabamd.lib()
     for n in sorted(names):
         assert hasattr(lib, n), n
-    assert lib.dabgpu_abi_version() == 6
+    assert lib.dabgpu_abi_version() == 7
 
 
 def test_abi_fails_loudly_without_device():

@@ -11,6 +11,8 @@ for r in $(seq 1 $reps); do
         > gpurun_out/ab_${n}_$r.log 2>&1 || { echo "$n failed"; tail -5 gpurun_out/ab_${n}_$r.log; exit 1; }
     grep '"value"' gpurun_out/ab_${n}_$r.log | python3 -c "
 import json,sys; d=json.loads(sys.stdin.read()); k=d['kernel_ms_per_launch']
-print('$n rep $r value %.4g M ms/step %.3f acs %.3f demod %.3f tb %.3f dabplus %.3f' % (d['value']/1e6, d['ms_per_step'], k['msc_acs'], k['demod'], k['msc_traceback'], k['dabplus']))"
+a=d.get('kernel_ms_per_launch_alone') or {}
+print('$n rep $r value %.4g M ms/step %.3f acs %.3f demod %.3f tb %.3f dabplus %.3f' % (d['value']/1e6, d['ms_per_step'], k['msc_acs'], k['demod'], k['msc_traceback'], k['dabplus'])
+      + (' | alone demod %.3f acs %.3f tb %.3f' % (a['demod'], a['msc_acs'], a['msc_traceback']) if a.get('demod') else ''))"
   done
 done
