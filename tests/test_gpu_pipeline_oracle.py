@@ -394,6 +394,22 @@ def test_packed_msc_output_and_dabplus_match_reference_path(ctx, pad, fmt, packe
     assert ok3 > 0
 
 
+@pytest.mark.parametrize("packed", [False, "fic"], ids=["bits", "fib_bytes"])
+def test_fic_only_pipeline_matches_reference_path(ctx, packed):
+    """a pipeline that decodes no subchannel: the FIC alone through its own ACS and
+    traceback launches (not the MSC's shared ones) and k_fic_post -- FIC bits (or, with
+    DABGPU_PACK_FIC, FIB bytes: the traceback's packed stores at a 96-byte row stride and the
+    CRC check on bytes) and CRC flags equal the reference path's, near the threshold"""
+    F, runs = 4, 3
+    iqs = _gen(MIXED, F * runs + 1, [41, 42], 9.0, fmt=S16)
+    refs = orc.decode_streams(iqs, F * runs, MIXED)
+    gpu = pc.gpu_decode(ctx, iqs, F, runs, [], packed=packed, iq_format=S16)
+    for s in range(2):
+        st = pc.compare(gpu[s], refs[s], [], check_soft=False)
+        _check([st], ("fic only", packed, s), soft=False)
+        assert st["fic_cw"] == 4 * st["frames"] and st["msc_cw"] == 0
+
+
 @pytest.mark.parametrize("fmt", [S16, U8], ids=["s16", "u8"])
 def test_recorded_format_decodes_like_converted_cf32(ctx, fmt):
     """the pipeline reading .sdr / .raw samples straight from HBM (the conversion inside
