@@ -617,8 +617,17 @@ def main():
     pipe.sync()
     acquire_ms = (time.perf_counter() - t_acq) * 1e3
 
-    def step(k, download=False):
-        r = pipe.run(diq, stride, [stride] * E, download=download)
+    def step(k, download=False, partial=False):
+        try:
+            r = pipe.run(diq, stride, [stride] * E, download=download, partial=partial)
+        except dabamd.DabError:
+            # which stream, where: every stream's state to stderr before the error ends the run
+            for s in range(E):
+                x = pipe.state(s)
+                print(f"rank {rank} step {k} stream {s}: next_pos {x.next_pos} of {stride} "
+                      f"frames_run {x.frames_run} cif_count {x.cif_count} synced {x.synced} "
+                      f"acquiring {x.acquiring} resyncs {x.resyncs} acquisitions {x.acquisitions}", file=sys.stderr)
+            raise
         d = pipe.dabplus(download=download) if dabplus else None
         return r, d
 
@@ -1090,11 +1099,13 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
     for mode in ("sync", "async"):
         pipe.sync()
         pipe.control(dabamd.CTL_ACQ_ASYNC if mode == "async" else dabamd.CTL_ACQ_SYNC)
-        step(k0)                                           # untimed
+        # partial: a stream may not get back (below) -- the run still delivers the others
+        step(k0, partial=True)                             # untimed
         k0 += 1
         frames0 = [pipe.state(s).cif_count // 4 for s in range(E)]
         pos0 = [pipe.state(s).next_pos for s in range(E)]
         losses = 0
+        jammed = []
         for i in range(0, steps, 2):
             # stream j: the interferer half-way through the frames of step k0 + i + 1
             s = j % E
@@ -1102,12 +1113,18 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
             if at + n < stride:
                 diq.upload_at(jam, (s * stride + at) * bps)
                 losses += 1
+                jammed.append(s)
             j += 1
         pipe.sync()
         barrier(dist)
         t0 = time.perf_counter()
         for i in range(steps):
-            step(k0 + i)
+            # A stream whose search starts where the end of a null is detected just too late
+            # (the PRS's first 50 samples below 0.75 sLevel) restarts every T_F and can lock
+            # onto the frame period for good -- the reference's ofdmProcessor::run does the
+            # same on the same samples (the oracle never re-acquires either): that stream
+            # runs out of samples, the others go on (partial)
+            step(k0 + i, partial=True)
         pipe.sync()
         el = allreduce_max(dist, time.perf_counter() - t0)
         barrier(dist)
@@ -1115,7 +1132,8 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
         st = [pipe.state(s) for s in range(E)]
         frames = sum(st[s].cif_count // 4 - frames0[s] for s in range(E))
         ms = el / steps * 1e3
-        res[mode] = {"steps": steps, "losses": losses, "ms_per_step": ms,
+        lost = [s for s in jammed if not st[s].synced or st[s].acquiring or st[s].next_pos + TF > stride]
+        res[mode] = {"steps": steps, "losses": losses, "ms_per_step": ms, "streams_not_back": len(lost),
                      "hit_ms_per_loss": (ms - base_ms) * steps / max(losses, 1),
                      "hit_steps_per_loss": (ms - base_ms) * steps / max(losses, 1) / base_ms,
                      "frames_decoded": int(frames), "frames_loss_free": E * F * steps,
@@ -1127,7 +1145,11 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
     res["note"] = ("one stream every 2 steps loses sync (interferer over 1.5 frames, findIndex fails); sync "
                    "(DABGPU_CTL_ACQ_SYNC, the reference's order): the run waits for its null search (k_acquire); "
                    "async (DABGPU_CTL_ACQ_ASYNC, the engine's default since round 6): the search runs in the background "
-                   "and that stream rejoins a later run (its frames delivered later, frame for frame the same)")
+                   "and that stream rejoins a later run (its frames delivered later, frame for frame the same); "
+                   "streams_not_back: this rank's jammed streams not synchronised at the end of the leg (async: "
+                   "a search may still run; sync: a stream whose search locked onto the frame period -- the end of "
+                   "the null detected just after T_null + 50 samples at every attempt -- and ran out of samples, as "
+                   "the reference's ofdmProcessor::run does on the same samples)")
     return res
 
 

@@ -410,6 +410,23 @@ def test_fic_only_pipeline_matches_reference_path(ctx, packed):
         assert st["fic_cw"] == 4 * st["frames"] and st["msc_cw"] == 0
 
 
+def test_pipeline_null_lock_like_reference(ctx):
+    """the stream on which the reference's null search locks onto the frame period after a
+    sync loss (tests/null_lock.py, test_null_search_locks_onto_frame_period_like_reference):
+    with the reference's in-run search (ACQ_SYNC) the pipeline decodes the same 229 frames
+    as the oracle's ofdmProcessor::run -- placement, FIC bits, CRCs -- and is still not
+    synchronised when the stream's samples end"""
+    import null_lock as nl
+    _, x = nl.stream()
+    ref = orc.decode_streams([x], nl.FRAMES, [])[0]
+    assert ref["n"] == 229
+    gpu = pc.gpu_decode(ctx, [x], 8, 32, [], iq_format=S16, acq="sync")[0]
+    st = pc.compare(gpu, ref, [], check_soft=False)
+    _check([st], "null lock", soft=False)
+    assert st["frames"] == 229 and gpu["info"][-1].window == nl.LAST_WINDOW
+    assert not gpu["states"][-1].synced
+
+
 @pytest.mark.parametrize("fmt", [S16, U8], ids=["s16", "u8"])
 def test_recorded_format_decodes_like_converted_cf32(ctx, fmt):
     """the pipeline reading .sdr / .raw samples straight from HBM (the conversion inside
