@@ -1132,9 +1132,9 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
         st = [pipe.state(s) for s in range(E)]
         frames = sum(st[s].cif_count // 4 - frames0[s] for s in range(E))
         ms = el / steps * 1e3
-        # lost for good: out of samples, or neither synchronised nor searching (a search still
-        # running at the end of the leg is acquiring_at_end)
-        lost = [s for s in jammed if st[s].next_pos + TF > stride or not (st[s].synced or st[s].acquiring)]
+        # lost for good: a search that reached the end of the stream's samples (a search still
+        # running at the end of the leg is acquiring_at_end; one that found its null resumes)
+        lost = [s for s in jammed if st[s].next_pos + TF > stride]
         res[mode] = {"steps": steps, "losses": losses, "ms_per_step": ms, "streams_not_back": len(lost),
                      "hit_ms_per_loss": (ms - base_ms) * steps / max(losses, 1),
                      "hit_steps_per_loss": (ms - base_ms) * steps / max(losses, 1) / base_ms,
@@ -1148,11 +1148,10 @@ def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, b
                    "(DABGPU_CTL_ACQ_SYNC, the reference's order): the run waits for its null search (k_acquire); "
                    "async (DABGPU_CTL_ACQ_ASYNC, the engine's default since round 6): the search runs in the background "
                    "and that stream rejoins a later run (its frames delivered later, frame for frame the same); "
-                   "streams_not_back: this rank's jammed streams lost for good by the end of the leg (out of "
-                   "samples, or neither synchronised nor searching: a search that locked onto the frame period -- "
-                   "the end of the null detected just after T_null + 50 samples at every attempt -- as the "
-                   "reference's ofdmProcessor::run does on the same samples); searches still running are "
-                   "acquiring_at_end")
+                   "streams_not_back: this rank's jammed streams whose search reached the end of their samples "
+                   "(it locked onto the frame period -- the end of the null detected just after T_null + 50 samples "
+                   "at every attempt -- as the reference's ofdmProcessor::run does on the same samples); searches "
+                   "still running at the end of the leg are acquiring_at_end")
     return res
 
 
