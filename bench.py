@@ -537,6 +537,9 @@ def main():
     ap.add_argument("--solo-steps", type=int, default=2,
                     help="steps after the timed region with every kernel alone on the device (profiling mode 3): "
                          "per-kernel times without overlap, to name the dominant kernel")
+    ap.add_argument("--delivered-mode", choices=["fetch", "direct"], default="fetch",
+                    help="delivered leg: copies behind the decoding (dabgpu_pipe_fetch) or the decoders writing "
+                         "pinned host memory directly")
     ap.add_argument("--delivered-fic", choices=["bytes", "bits"], default="bytes",
                     help="FIC format of the delivered leg: FIB bytes (DABGPU_PACK_FIC) or one bit per byte")
     ap.add_argument("--delivered-steps", type=int, default=10,
@@ -681,7 +684,7 @@ def main():
     if deliv_steps:
         k0 = ck + 1 + args.solo_steps
         delivered = delivered_leg(dabamd, ctx, pipe, step, k0, deliv_steps - 1, E, F, SUBCH, dabplus, dist, truth, P,
-                                  fic_bytes=args.delivered_fic == "bytes")
+                                  fic_bytes=args.delivered_fic == "bytes", direct=args.delivered_mode == "direct")
     sync_loss = None
     if loss_steps and E >= 2:
         k0 = ck + 1 + args.solo_steps + deliv_steps
@@ -1008,10 +1011,28 @@ def c4_fed_leg(dabamd, ctx, dist, rank, world, local, E, F, subs, SUBCH, dabplus
                     "kernels' loads).  Link-bound by design: DESIGN.md section 7"}
 
 
-def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist, truth, P, fic_bytes=True):
+class _HostOut:
+    """pinned host memory (dabgpu_host_alloc) as a pipeline output buffer: the kernels write it
+    through its device address (hipHostGetDevicePointer; the same address under ROCm's unified
+    addressing, asked anyway)"""
+
+    def __init__(self, hb):
+        import ctypes as C
+        hip = C.CDLL("libamdhip64.so")
+        d = C.c_void_p()
+        if hip.hipHostGetDevicePointer(C.byref(d), hb.ptr, 0) != 0 or not d.value:
+            raise RuntimeError("pinned host buffer has no device address")
+        self.hb, self.ptr = hb, d
+
+
+def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist, truth, P, fic_bytes=True,
+                  direct=False):
     """`steps` timed steps whose outputs are copied to pinned host memory (two sets,
     alternating like the pipeline's device outputs), each copy on its run's back-end
-    stream behind the channel decoding (dabgpu_pipe_fetch), overlapping the next run.
+    stream behind the channel decoding (dabgpu_pipe_fetch), overlapping the next run --
+    or (direct) written there by the decoders themselves: the run's FIC, CRC and MSC
+    output pointers are dabgpu_host_alloc memory (zero copy; not with DAB+ subchannels,
+    whose layer reads the MSC bytes back).
     The last step's host copy of ensemble 0 is checked against the transmitted bits."""
     pipe.sync()
     msc_packed = pipe.packed
@@ -1026,11 +1047,20 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
     n_sfi = E * 4 * F * nd * 16 if nd else 0                     # dabgpu_superframe records
     n_sf = E * nd * pipe.sf_slots * pipe.sf_stride if nd else 0  # compact: DABGPU_SF_SLOTS per subchannel
     total = n_fic + n_crc + n_msc + n_sfi + n_sf
-    hb = [dabamd.HostBuf(ctx, total) for _ in range(2)]
+    direct = direct and not nd
+    if direct:
+        hb = [dabamd.HostBuf(ctx, n) for _ in range(2) for n in (n_fic, n_crc, n_msc)]
+        saved = pipe._outs
+        pipe._outs = [tuple(_HostOut(hb[3 * q + r]) for r in range(3)) for q in range(2)]
+    else:
+        hb = [dabamd.HostBuf(ctx, total) for _ in range(2)]
     valids = [None, None]
 
     def one(k, i):
         valid, _ = step(k)
+        valids[i & 1] = valid
+        if direct:
+            return
         h = hb[i & 1]
         o = 0
         for src, n in ((pipe.fic_d, n_fic), (pipe.crc_d, n_crc), (pipe.msc_d, n_msc)) + \
@@ -1038,7 +1068,6 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
             if n:
                 pipe.fetch(h, src, n, o)
             o += n
-        valids[i & 1] = valid
 
     one(k0, 0)                                                  # untimed: the packed format's first run
     pipe.sync()
@@ -1052,16 +1081,25 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
     el = allreduce_max(dist, time.perf_counter() - t0)
     barrier(dist)
     st1 = pipe.state(0)
-    h = hb[steps & 1]
-    fic = h.view(np.uint8, (E, F, 4, fb))
+    if direct:                                                  # the last run's own buffers
+        fic = pipe.fic_d.hb.view(np.uint8, (E, F, 4, fb))
+        crc = pipe.crc_d.hb.view(np.uint8, (E, F, 12))
+        msc = pipe.msc_d.hb.view(np.uint8, (E, 4 * F, ns, pipe.msc_stride_packed))
+    else:
+        h = hb[steps & 1]
+        fic = h.view(np.uint8, (E, F, 4, fb))
+        crc = h.view(np.uint8, (E, F, 12), n_fic)
+        msc = h.view(np.uint8, (E, 4 * F, ns, pipe.msc_stride_packed), n_fic + n_crc)
     if fic_bytes:
         fic = np.unpackbits(fic, axis=-1)
-    crc = h.view(np.uint8, (E, F, 12), n_fic)
-    msc = np.unpackbits(h.view(np.uint8, (E, 4 * F, ns, pipe.msc_stride_packed), n_fic + n_crc), axis=-1)
+    msc = np.unpackbits(msc, axis=-1)
     check = check_step(truth, P, st0, st1, fic, crc, msc, valids[steps & 1], subch)
+    pipe.sync()
+    if direct:
+        pipe._outs = saved
+        pipe.fic_d, pipe.crc_d, pipe.msc_d = saved[0]
     for b in hb:
         b.free()
-    pipe.sync()
     pipe.set_packed(dabamd.PACK_MSC if msc_packed else 0)      # the timed legs' format again
     if nd:
         pipe.set_dabplus_compact(False)
@@ -1070,11 +1108,13 @@ def delivered_leg(dabamd, ctx, pipe, step, k0, steps, E, F, subch, dabplus, dist
             "bytes_to_host_per_step": total, "pcie_GBps": total * steps / el / 1e9,
             "msc_format": "8 bits per byte, msb first (dabgpu_pipe_set_packed)",
             "fic_format": "FIB bytes, 96 per FIC block (DABGPU_PACK_FIC)" if fic_bytes else "1 bit per byte",
-            "checked_last_step_from_host_memory": check,
+            "checked_last_step_from_host_memory": check, "mode": "direct" if direct else "fetch",
             "note": "FIC + CRC flags + packed MSC bytes" + (" + DAB+ superframe records and the run's "
                                                                  "superframe bytes (compact)" if nd else "")
-                    + " of every step copied to pinned host memory behind its run's channel decoding "
-                      "(dabgpu_pipe_fetch), overlapping the next run"}
+                    + (" of every step written to pinned host memory by the decoders themselves (the run's "
+                       "output pointers are dabgpu_host_alloc memory)" if direct else
+                       " of every step copied to pinned host memory behind its run's channel decoding "
+                       "(dabgpu_pipe_fetch), overlapping the next run")}
 
 
 def sync_loss_leg(dabamd, ctx, pipe, step, k0, steps, E, F, stride, diq, dist, base_ms, fmt="f32"):
