@@ -320,8 +320,12 @@ int dabgpu_pipe_acquire(dabgpu_pipe *p, const void *iq_d, int64_t stream_stride,
 /* Decode the next n_frames frames of every stream, as ofdmProcessor::run does:
  * a stream whose findIndex fails goes back to the null-symbol search from where it
  * is (goto notSynced, ofdm-processor.cpp:354-357) and continues with the frames
- * after it.  Outputs (device):
- *   fic_bits_d  [n_streams][n_frames][4][768], fic_crc_d [n_streams][n_frames][12]
+ * after it.  Outputs (device memory, or dabgpu_host_alloc memory through its device
+ * address: the decoders then write across PCIe themselves -- zero copy, slower than
+ * dabgpu_pipe_fetch behind the decoding on MI355X; not for a pipeline with DAB+
+ * subchannels, whose layer reads msc_bits_d back):
+ *   fic_bits_d  [n_streams][n_frames][4][768] (DABGPU_PACK_FIC: [4][96] FIB bytes),
+ *               fic_crc_d [n_streams][n_frames][12]
  *               (frame f of stream s: its f-th frame of this run; frames past
  *               dabgpu_stream_state.frames_run have CRC flags 0)
  *   msc_bits_d  [n_streams][4*n_frames][n_subch][msc_stride] (24*bitRate used)

@@ -818,6 +818,58 @@ def test_fetch_to_host_equals_download(ctx):
             b.free()
 
 
+def test_outputs_in_pinned_host_memory_equal_device_outputs(ctx):
+    """dabgpu_pipe_run's FIC / CRC / MSC outputs may be dabgpu_host_alloc memory (zero copy:
+    the traceback and k_fic_post write across PCIe, bench.py --delivered-mode direct): over
+    runs with packed MSC and FIB bytes, the bytes equal a second pipeline's device outputs"""
+    import ctypes as C
+    import dabamd
+    sub = MIXED[:3]
+    F, runs = 4, 3
+    iqs = _gen(sub, F * runs + 1, [81, 82], 15.0)
+    S = len(iqs)
+    lens = [len(x) // 2 for x in iqs]
+    stride = max(lens)
+    buf = np.zeros((S, 2 * stride), np.float32)
+    for s, x in enumerate(iqs):
+        buf[s, :len(x)] = x
+    diq = ctx.put(buf)
+    subs = [dabamd.Subch(sc[0], sc[1], sc[2], sc[3], 0 if sc[4] else 1, 0) for sc in sub]
+    pa, pb = dabamd.Pipeline(ctx, S, F, subs), dabamd.Pipeline(ctx, S, F, subs)
+    hip = C.CDLL("libamdhip64.so")
+
+    class Out:                      # a pinned host buffer through its device address
+        def __init__(self, n):
+            self.hb = dabamd.HostBuf(ctx, n)
+            d = C.c_void_p()
+            assert hip.hipHostGetDevicePointer(C.byref(d), self.hb.ptr, 0) == 0 and d.value
+            self.ptr = d
+    n_fic, n_crc = S * F * 4 * 96, S * F * 12
+    n_msc = S * 4 * F * len(sub) * pa.msc_stride_packed
+    outs = [(Out(n_fic), Out(n_crc), Out(n_msc)) for _ in range(2)]
+    dev = pb._outs                  # pb's own device buffers, freed by close()
+    try:
+        for p in (pa, pb):
+            p.set_packed(dabamd.PACK_MSC | dabamd.PACK_FIC)
+        pb._outs = outs
+        for r in range(runs):
+            pa.run(diq, stride, lens, download=False, partial=True)
+            pb.run(diq, stride, lens, download=False, partial=True)
+            pa.sync()
+            pb.sync()
+            for d, h, n in ((pa.fic_d, pb.fic_d, n_fic), (pa.crc_d, pb.crc_d, n_crc), (pa.msc_d, pb.msc_d, n_msc)):
+                assert np.array_equal(d.download(np.uint8, (n,)), h.hb.view(np.uint8, (n,))), r
+            assert pb.fic_d.hb.view(np.uint8, (n_fic,)).any()
+    finally:
+        pb._outs = dev
+        pa.close()
+        pb.close()
+        for o in outs:
+            for b in o:
+                b.hb.free()
+        diq.free()
+
+
 def test_dabplus_compact_output_equals_sparse(ctx):
     """dabgpu_pipe_set_dabplus_compact: the run's decoded superframes in CIF order, slot k
     of the k-th, the record's `reserved` = k -- the same bytes and records as the sparse
